@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""SpMV benchmark on MI355X — BASELINE.json metric "SpMV GFLOP/s + effective HBM GB/s
+(% roofline), fp64, 1/2/4/8 MI355X".
+
+A step = one y = A*x over the workload's matrix, through the C-ABI plan (spmv_plan_run: the
+flagged-tile kernel + its fix-up), with A, x and y resident in HBM before the timed region.
+
+Workloads:
+  powerlaw (default, config 3): n = m = 10,000,000, nnz = 160,000,000, Pareto(2) row lengths
+      (mean 16, max ~2e4), columns spread over [0,m), fp64. BASELINE's target is quoted here.
+  banded   (config 2): n = m = 1,000,000, 16 nnz/row.
+  --dtype f32 (config 5): the power-law matrix in fp32.
+Multi-GPU (--gpus N, one process per GPU, torch.distributed over RCCL):
+  --scaling weak (default): rank r owns its own 10M-row / 160M-nnz row partition of an
+      (N*10M) x 10M matrix; x replicated; no collective inside the timed step (SURVEY §8e rows
+      are independent); value = total nnz of all ranks * 2 / max-over-ranks time.
+  --scaling strong (config 4): the single 10M/160M matrix split in nnz-balanced row slices.
+  The y exchange (RCCL reduce of partials = accum_results semantics, and RCCL gather of the
+  disjoint slices) is timed separately and reported in "exchange".
+
+Extra JSON fields: roofline (dominant kernel k_spmv_tiles, HIP events on its launch stream),
+cpu_baseline (the oracle's restatement of spmv_gold, 1 thread, on the host of the GPU box),
+parity (full-size componentwise-scaled error vs that oracle run).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "spmv-fpga_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import spmv_dist  # noqa: E402
+import spmv_hw  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["powerlaw", "banded"], default="powerlaw")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--nnz", type=int, default=None)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC traffic summary written by tools/pmc_traffic.py")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def build_workload(lib, args, world, rank):
+    """Returns (row_ptr, col, val, x, nr_cols, desc, rows_begin) on this rank's GPU."""
+    if args.workload == "banded":
+        n = args.rows or 1_000_000
+        rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2 + 1000 * rank)
+        x = spmv_hw.gen_vector(lib, n, seed=3)
+        desc = {"workload": "banded", "rows": n, "cols": n, "nnz_per_row": 16, "nnz": n * 16}
+        return rp, col, val, x, n, desc
+    n = args.rows or 10_000_000
+    z = args.nnz or 160_000_000
+    if world > 1 and args.scaling == "strong":
+        rp_full, _ = lib.powerlaw_row_ptr(n, z, 65536, 4)
+        b = lib.partition_rows(rp_full, world)
+        r0, r1 = spmv_dist.row_slice(b, rank)
+        rp, col, val, scale = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4, row_begin=r0, row_end=r1)
+        desc = {"workload": "powerlaw", "rows": n, "cols": n, "nnz": z, "slice_rows": [r0, r1]}
+    else:
+        # weak: rank r's own 10M-row partition (row-length seed 4 + 1000r, columns of global rows)
+        rp, col, val, scale = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4 + 1000 * rank)
+        desc = {"workload": "powerlaw", "rows": n, "cols": n, "nnz": z}
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    desc.update({"alpha": 2.0, "scale": round(scale, 4), "mean_nnz_per_row": z / n})
+    return rp, col, val, x, n, desc
+
+
+def cpu_baseline(lib, rp, col, val, x, y_gpu, reps):
+    """Times the oracle's restatement of spmv_gold (1 thread, -O2 -ffp-contract=off) on the
+    same matrix in host memory, and checks the full-size GPU result against it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    h_rp = rp.cpu().numpy().view(np.uint32)
+    h_col = col.cpu().numpy().view(np.uint32)
+    h_val = val.cpu().numpy()
+    h_x = x.cpu().numpy()
+    n = len(h_rp) - 1
+    y = np.zeros(n, h_val.dtype)
+    times = []
+    for _ in range(max(1, reps)):
+        t0 = time.perf_counter()
+        oracle.spmv_gold_rows(h_rp, h_col, h_val, h_x, 0, n, out=y)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    nnz = int(h_rp[-1])
+    err = oracle.scaled_error(h_rp, h_col, h_val, h_x, y, y_gpu.cpu().numpy())
+    abs_errors = oracle.verification_errors(y, y_gpu.cpu().numpy().astype(h_val.dtype))
+    try:
+        model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    base = {"value": round(2.0 * nnz / t / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
+            "sample": f"full matrix ({n} rows, {nnz} nnz), median of {len(times)} runs, "
+                      f"{t * 1e3:.1f} ms/SpMV, oracle/csr_ref.c spmv_gold, host {model}, "
+                      f"nproc {os.cpu_count()}"}
+    parity = {"max_scaled_err": err, "tol": 1e-6 if h_val.dtype == np.float64 else 1e-4,
+              "ref_abs_1e-5_errors": abs_errors, "pass": bool(err <= (1e-6 if h_val.dtype == np.float64 else 1e-4))}
+    return base, parity
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dtype = np.float64 if args.dtype == "f64" else np.float32
+    lib = spmv_hw.load(dtype)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream()
+
+    t_setup = time.perf_counter()
+    rp, col, val, x, ncols, desc = build_workload(lib, args, world, rank)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, ncols, device=local, stream=stream)
+    st = plan.stats()
+    y = torch.empty(st["nr_rows"], dtype=x.dtype, device=dev)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+    keep_csr = rank == 0 and world == 1 and not args.no_cpu
+    if not keep_csr:
+        del rp, col, val
+        torch.cuda.empty_cache()
+
+    for _ in range(args.warmup):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+
+    barrier(world)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    kernel_ms, _, launches = plan.timing()
+    plan.set_timing(False)
+    ms_local = (t1 - t0) * 1e3 / args.steps
+    ms = spmv_dist.max_over_ranks(ms_local, dev)
+    kernel_ms_max = spmv_dist.max_over_ranks(kernel_ms, dev)
+
+    nnz_local = st["nr_nzeros"]
+    alg_local = st["algorithmic_bytes"]
+    t_nnz = torch.tensor([float(nnz_local), float(alg_local)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_nnz)
+    nnz_all, alg_all = float(t_nnz[0]), float(t_nnz[1])
+    if world > 1 and args.scaling == "strong":
+        # one matrix: x and the row_ptr sentinel count once, not once per rank
+        alg_all -= (world - 1) * (st["nr_cols"] * np.dtype(dtype).itemsize + 4)
+
+    gflops = 2.0 * nnz_all / (ms * 1e-3) / 1e9
+    eff_gbps = alg_all / (ms * 1e-3) / 1e9
+    # roofline of the dominant kernel: algorithmic bytes of one launch / mean launch duration
+    achieved = alg_local / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tr = json.load(open(args.traffic))
+            key = f"{desc['workload']}_{args.dtype}"
+            if key in tr and tr[key].get("nnz") == nnz_local:
+                traffic = tr[key]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+
+    exchange = None
+    if world > 1:
+        counts = None
+        t_cnt = torch.zeros(world, dtype=torch.int64, device=dev)
+        t_cnt[rank] = st["nr_rows"]
+        dist.all_reduce(t_cnt)
+        counts = t_cnt.cpu().numpy()
+        row_begin = int(counts[:rank].sum())
+        n_total = int(counts.sum())
+        res = {}
+        for mode in ("gather", "reduce"):
+            for _ in range(2):  # warm the communicator
+                (spmv_dist.exchange_gather(y, counts) if mode == "gather"
+                 else spmv_dist.exchange_reduce(y, row_begin, n_total))
+            torch.cuda.synchronize()
+            barrier(world)
+            reps = 5
+            te0 = time.perf_counter()
+            for _ in range(reps):
+                (spmv_dist.exchange_gather(y, counts) if mode == "gather"
+                 else spmv_dist.exchange_reduce(y, row_begin, n_total))
+            torch.cuda.synchronize()
+            barrier(world)
+            res[f"{mode}_ms"] = round(spmv_dist.max_over_ranks((time.perf_counter() - te0) * 1e3 / reps, dev), 4)
+        res["y_bytes"] = n_total * y.element_size()
+        res["e2e_gflops_with_gather"] = round(2.0 * nnz_all / ((ms + res["gather_ms"]) * 1e-3) / 1e9, 2)
+        exchange = res
+
+    cpu = None
+    parity = None
+    if keep_csr:
+        cpu, parity = cpu_baseline(lib, rp, col, val, x, y, args.cpu_reps)
+
+    if rank == 0:
+        out = {
+            "metric": "SpMV GFLOP/s + effective HBM GB/s (% roofline), fp64, 1/2/4/8 MI355X",
+            "value": round(gflops, 3),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": args.scaling if world > 1 else "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (splitmix64 generator, SURVEY.md §8d)",
+            "config": dict(desc, parallelism=f"row-slice x{world}", dtype=args.dtype),
+            "effective_GBps": round(eff_gbps, 2),
+            "roofline_pct": round(100.0 * eff_gbps / (HBM_PEAK_GBPS * world), 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel": "k_spmv_tiles", "kernel_ms": round(kernel_ms, 5),
+                         "kernel_launches": launches, "alg_bytes_per_launch": alg_local},
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "exchange": exchange,
+            "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "nr_nonempty_rows")},
+            "setup_s": round(setup_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    plan.destroy()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

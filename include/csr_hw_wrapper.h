@@ -1,0 +1,129 @@
+/*
+ * csr_hw_wrapper.h — C-ABI of libspmv_hw_{f64,f32}.so, the MI355X drop-in for the reference's
+ * FPGA path (csr_hw_wrapper.cpp + csr_hw.cpp + spmv.cpp of euroexa/spmv-fpga).
+ *
+ * Part 1 — the reference API, same names / argument meaning / ownership
+ * -------------------------------------------------------------------
+ *   create_csr_hw_matrix     replaces csr_hw_wrapper.h:9,   csr_hw_wrapper.cpp:3-80
+ *   create_csr_hw_y_vector   replaces csr_hw_wrapper.h:10,  csr_hw_wrapper.cpp:82-185
+ *   create_csr_hw_x_vector   replaces csr_hw_wrapper.h:11,  csr_hw_wrapper.cpp:187-191
+ *   spmv_hw                  replaces csr_hw_wrapper.h:13,  csr_hw_wrapper.cpp:193-288
+ *   delete_csr_hw_matrix     replaces csr_hw_wrapper.h:15,  csr_hw_wrapper.cpp:291-296
+ *   delete_csr_hw_y_vector   replaces csr_hw_wrapper.h:16,  csr_hw_wrapper.cpp:298-303
+ *   delete_csr_hw_x_vector   replaces csr_hw_wrapper.h:17,  csr_hw_wrapper.cpp:305-308
+ *   storage_overhead         replaces csr_hw.h:140,         csr_hw.cpp:1401-1409
+ *   verification             replaces csr_hw.h:148,         csr_hw.cpp:1571-1590
+ *
+ * Semantics kept from the reference:
+ *   - *hw_matrix is a malloc'd array of spmv_hw_units() handles ("ComputeUnits", util.h:41-59),
+ *     one per unit; each handle's public fields are valid host memory (main.cpp:69,86-87).
+ *   - *empty_rows_bitmap is malloc'd; the caller frees ONLY the outer array (main.cpp:95). Here
+ *     the inner rows live inside the same allocation, so that free() releases everything.
+ *   - spmv_hw is synchronous and ACCUMULATES (+=) into y_fpga->values (csr_hw.cpp:1555,
+ *     main.cpp:74 hands in a zeroed vector). It prints the same three timing lines
+ *     (csr_hw_wrapper.cpp:274,284-285).
+ *   - verification: absolute threshold 1e-5, NaN counts as an error (csr_hw.cpp:1573-1580).
+ *   - storage_overhead: MB of one unit's hw representation; computed in 64 bits (the reference
+ *     sums in 32-bit IndexType and overflows past 512 MB).
+ * Error behaviour: the reference has no error channel (all void, nothing checked). This library
+ * fails fast: a HIP error or invalid input prints "spmv_hw: <what>" to stderr and exit(1)s, for
+ * the Part-1 API. Part 2 returns error codes instead and records spmv_hw_last_error().
+ *
+ * Part 2 — device-resident extensions (used by bench.py, the tests and multi-process runs)
+ * -------------------------------------------------------------------------------------
+ *   A spmv_plan is ONE unit's matrix slice in the MI355X hw representation.
+ *   Pointers named d_* are device addresses on the plan's device; `stream` is a hipStream_t
+ *   (NULL = default stream). All Part-2 calls return 0 on success, nonzero on error.
+ */
+#ifndef CSR_HW_WRAPPER_H
+#define CSR_HW_WRAPPER_H
+
+#include "spmv_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- Part 1: reference API ---------------- */
+void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool ***empty_rows_bitmap);
+void create_csr_hw_y_vector(csr_hw_matrix **hw_matrix, csr_hw_vector ***hw_vector);
+void create_csr_hw_x_vector(csr_hw_vector **hw_x, csr_vector *x, int blocks, IndexType *nr_cols);
+void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga, bool **empty_rows_bitmap);
+void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix);
+void delete_csr_hw_y_vector(csr_hw_vector **hw_vector);
+void delete_csr_hw_x_vector(csr_hw_vector *hw_vector);
+ValueType storage_overhead(csr_hw_matrix *matrix);
+int verification(IndexType nr_values, ValueType *sw_values, ValueType *hw_values, int verbose);
+
+/* ---------------- Part 2: extensions ---------------- */
+
+/* Number of units ("ComputeUnits"): env SPMV_NGPUS (default 1). Unit u runs on HIP device
+ * (u % device_count); more units than devices gives virtual units sharing a GPU. */
+int spmv_hw_units(void);
+/* Bytes of sizeof(ValueType) this library was built for (8 = DOUBLE=1, 4 = DOUBLE=0). */
+int spmv_hw_value_bytes(void);
+/* Last error message of a Part-2 call on this thread ("" if none). */
+const char *spmv_hw_last_error(void);
+
+typedef struct spmv_plan spmv_plan;
+
+typedef struct spmv_plan_stats {
+    uint64_t nr_rows;            /* rows of the slice */
+    uint64_t nr_cols;            /* columns (length of x) */
+    uint64_t nr_nzeros;          /* stored non-zeros */
+    uint64_t nr_nonempty_rows;   /* rows with >= 1 non-zero */
+    uint64_t nr_tiles;           /* wave tiles of the main kernel */
+    uint64_t tile_nnz;           /* non-zeros per wave tile */
+    uint64_t device_bytes;       /* bytes of the hw representation resident in HBM */
+    uint64_t algorithmic_bytes;  /* compulsory CSR bytes per SpMV, SURVEY.md §8(d) */
+    int32_t device;              /* HIP device ordinal */
+    int32_t kernel;              /* 0 = flagged-tile gather, 1 = flagged-tile LDS x-window */
+    int32_t blocks;              /* column blocks of the representation */
+    int32_t lds_tiles_pct;       /* % of tiles served from an LDS x-window (kernel 1) */
+} spmv_plan_stats;
+
+/* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are
+ * rebased to d_row_ptr[0]). The CSR arrays are only read; the plan owns its own copies. */
+int spmv_plan_create_device(spmv_plan **plan, int device, IndexType nr_rows, IndexType nr_cols,
+                            IndexType nr_nzeros, const IndexType *d_row_ptr,
+                            const IndexType *d_col_ind, const ValueType *d_values, void *stream);
+/* Build a plan from rows [row_begin, row_end) of a host CSR matrix. */
+int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *matrix,
+                          IndexType row_begin, IndexType row_end);
+/* d_y[0:nr_rows) = A * d_x  (overwrite; empty rows get 0). Asynchronous on `stream`. */
+int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, void *stream);
+int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
+/* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
+ * stream: enable, then read back the mean duration (ms) and count of timed launches. */
+int spmv_plan_set_timing(spmv_plan *plan, int enable);
+int spmv_plan_get_timing(spmv_plan *plan, double *mean_ms, double *total_ms, int *launches);
+void spmv_plan_destroy(spmv_plan *plan);
+
+/* nnz-balanced contiguous row partition into `units` slices: bounds[0]=0, bounds[units]=nr_rows,
+ * slice u = rows [bounds[u], bounds[u+1]) with ~nnz/units non-zeros each (the
+ * reference's S1 rule, csr_hw.cpp:459, without the FPGA alignment rules S2/S3). Host only. */
+int spmv_partition_rows(const IndexType *row_ptr, IndexType nr_rows, int units, IndexType *bounds);
+
+/* ---------------- synthetic inputs (bench/test infrastructure) ---------------- */
+/* Banded: n x n, `width` non-zeros per row, columns [clamp(i - width/2, 0, n - width), +width),
+ * values U(-1,1) from splitmix64(seed). Writes d_row_ptr[n+1], d_col[n*width], d_val. */
+int spmv_gen_banded(IndexType n, IndexType width, uint64_t seed, IndexType *d_row_ptr,
+                    IndexType *d_col, ValueType *d_val, void *stream);
+/* Power-law row lengths (host): l_i = clamp(floor(s * u_i^-1/2), 1, max_len), s bisected so that
+ * sum(l) == nnz exactly (residual spread as +-1 over the last rows). Writes h_row_ptr[n+1]. */
+int spmv_gen_powerlaw_row_ptr(IndexType n, uint64_t nnz, IndexType max_len, uint64_t seed,
+                              IndexType *h_row_ptr, double *scale_out);
+/* Fill columns/values of rows [0,n) given d_row_ptr (device): row i with l non-zeros gets
+ * columns floor((j*m + r_ij) / l), r_ij = hash(seed,i,j) mod m (sorted, unique, spread over
+ * [0,m)), values U(-1,1). Row i's entries depend only on (seed, i + row_offset, l, m). */
+int spmv_gen_fill(IndexType n, IndexType m, uint64_t seed, uint64_t row_offset,
+                  const IndexType *d_row_ptr, IndexType *d_col, ValueType *d_val, void *stream);
+/* d_x[i] = lo + (hi-lo)*u_i, u_i = splitmix64(seed, i + offset) in [0,1). */
+int spmv_gen_vector(IndexType n, uint64_t seed, uint64_t offset, double lo, double hi,
+                    ValueType *d_x, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CSR_HW_WRAPPER_H */

@@ -1,0 +1,134 @@
+"""ctypes front-end of the CPU oracle (oracle/csr_ref.c). TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, as
+the checker. Parity status: "parity unpinned" (see csr_ref.c header and DESIGN.md §5).
+
+Each function names the reference code it restates (euroexa/spmv-fpga, src/...).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBS: dict = {}
+
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+
+
+def build() -> None:
+    """Compile liboracle_f64.so / liboracle_f32.so with gcc (oracle/Makefile)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib(dtype=np.float64) -> ctypes.CDLL:
+    dtype = np.dtype(dtype)
+    key = dtype.str
+    if key in _LIBS:
+        return _LIBS[key]
+    name = {np.dtype(np.float64): "liboracle_f64.so", np.dtype(np.float32): "liboracle_f32.so"}[dtype]
+    path = os.path.join(HERE, name)
+    if not os.path.exists(path):
+        build()
+    L = ctypes.CDLL(path)
+    vp = np.ctypeslib.ndpointer(dtype=dtype, flags="C_CONTIGUOUS")
+    cval = ctypes.c_double if dtype == np.float64 else ctypes.c_float
+    u32 = ctypes.c_uint32
+    L.oracle_read_csr_header.argtypes = [ctypes.c_char_p, ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                         ctypes.POINTER(u32), u32, ctypes.POINTER(ctypes.c_int)]
+    L.oracle_read_csr_matrix.argtypes = [ctypes.c_char_p, u32, u32, _u32p, _u32p, vp]
+    L.oracle_srand.argtypes = [ctypes.c_uint]
+    L.oracle_init_vector_rand.argtypes = [vp, u32, cval]
+    L.oracle_spmv_gold.argtypes = [u32, _u32p, _u32p, vp, vp, vp]
+    L.oracle_spmv_gold_rows.argtypes = [u32, u32, _u32p, _u32p, vp, vp, vp]
+    L.oracle_spmv_fpga_order.argtypes = [u32, u32, _u32p, _u32p, vp, vp, vp, u32, ctypes.c_int]
+    L.oracle_verification_errors.argtypes = [u32, vp, vp]
+    L.oracle_verification_errors.restype = ctypes.c_long
+    assert L.oracle_value_bytes() == dtype.itemsize
+    _LIBS[key] = L
+    return L
+
+
+def read_csr(path: str, dtype=np.float64, cols_div_blocks: int = 32768):
+    """csr.cpp:10-46 + :87-136 -> (nr_rows, nr_cols, row_ptr, col_ind, values, blocks)."""
+    L = lib(dtype)
+    r, c, z, b = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+    rc = L.oracle_read_csr_header(path.encode(), ctypes.byref(r), ctypes.byref(c), ctypes.byref(z),
+                                  cols_div_blocks, ctypes.byref(b))
+    if rc:
+        raise IOError(f"read_csr_header({path}) failed: {rc}")
+    row_ptr = np.zeros(r.value + 1, np.uint32)
+    col = np.zeros(z.value, np.uint32)
+    val = np.zeros(z.value, dtype)
+    rc = L.oracle_read_csr_matrix(path.encode(), r.value, z.value, row_ptr, col, val)
+    if rc:
+        raise IOError(f"read_csr_matrix({path}) failed: {rc}")
+    return r.value, c.value, row_ptr, col, val, b.value
+
+
+def init_vector_rand(n: int, dtype=np.float64, seed: int | None = 1, vmax: float = 1.0):
+    """csr.cpp:170-179 (libc rand(); the reference never seeds -> seed 1)."""
+    L = lib(dtype)
+    if seed is not None:
+        L.oracle_srand(seed)
+    x = np.zeros(n, dtype)
+    L.oracle_init_vector_rand(x, n, vmax)
+    return x
+
+
+def spmv_gold(row_ptr, col, val, x):
+    """csr.cpp:184-194: y[i] = sum_j val[j]*x[col[j]] accumulated from 0 in CSR order."""
+    dtype = val.dtype
+    n = len(row_ptr) - 1
+    y = np.zeros(n, dtype)
+    lib(dtype).oracle_spmv_gold(n, _c(row_ptr, np.uint32), _c(col, np.uint32), _c(val, dtype),
+                                _c(x, dtype), y)
+    return y
+
+
+def spmv_gold_rows(row_ptr, col, val, x, row_begin: int, row_end: int, out=None):
+    dtype = val.dtype
+    y = out if out is not None else np.zeros(row_end - row_begin, dtype)
+    lib(dtype).oracle_spmv_gold_rows(row_begin, row_end, row_ptr, col, val, x, y)
+    return y
+
+
+def spmv_fpga_order(row_ptr, col, val, x, nr_cols: int, cols_div_blocks: int, vf: int, y=None):
+    """Arithmetic order of spmv.cpp:66-104 + csr_hw.cpp:1531-1565 (accumulates into y)."""
+    dtype = val.dtype
+    n = len(row_ptr) - 1
+    if y is None:
+        y = np.zeros(n, dtype)
+    lib(dtype).oracle_spmv_fpga_order(n, nr_cols, _c(row_ptr, np.uint32), _c(col, np.uint32),
+                                      _c(val, dtype), _c(x, dtype), y, cols_div_blocks, vf)
+    return y
+
+
+def verification_errors(sw, hw) -> int:
+    """csr_hw.cpp:1571-1590: number of entries with |sw-hw| >= 1e-5 or NaN."""
+    dtype = sw.dtype
+    return int(lib(dtype).oracle_verification_errors(len(sw), _c(sw, dtype), _c(hw, dtype)))
+
+
+def scaled_error(row_ptr, col, val, x, y_ref, y_test) -> float:
+    """max_i |y_ref_i - y_test_i| / (|A||x|)_i  (SURVEY §8d parity metric; rows with
+    (|A||x|)_i == 0 must match exactly)."""
+    n = len(row_ptr) - 1
+    absax = np.zeros(n, np.float64)
+    lens = np.diff(row_ptr.astype(np.int64))
+    rows = np.repeat(np.arange(n), lens)
+    np.add.at(absax, rows, np.abs(val.astype(np.float64)) * np.abs(x.astype(np.float64)[col]))
+    diff = np.abs(y_ref.astype(np.float64) - y_test.astype(np.float64))
+    zero = absax == 0
+    if np.any(diff[zero] != 0) or np.any(np.isnan(diff)):
+        return float("inf")
+    if np.all(zero):
+        return 0.0
+    return float(np.max(diff[~zero] / absax[~zero]))
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)

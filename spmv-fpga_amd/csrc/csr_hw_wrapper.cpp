@@ -1,0 +1,356 @@
+// The reference API (csr_hw_wrapper.h:9-17, csr_hw.h:140,148) as a thin C-ABI shim over the
+// MI355X plans. One handle per unit ("Compute Unit" -> GPU, util.h:41-59); units own
+// contiguous nnz-balanced row slices (the role of prepare_balanced_hw_matrix's S1 split,
+// csr_hw.cpp:459). x is replicated on every GPU in use (the reference copies x into every CU's
+// BRAM, spmv.cpp:280-294). spmv_hw runs every unit's kernels, then adds each unit's y slice
+// into the caller's y_fpga (the role of accum_results, csr_hw.cpp:1531-1565, and the loop
+// csr_hw_wrapper.cpp:276-281), printing the reference's timing lines.
+#include <sys/time.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <iomanip>
+#include <iostream>
+#include <mutex>
+
+#include "spmv_internal.hpp"
+
+using namespace spmvhw;
+
+namespace {
+
+[[noreturn]] void die(const std::string &what)
+{
+    std::fprintf(stderr, "spmv_hw: %s\n", what.c_str());
+    std::fflush(stderr);
+    std::exit(1);
+}
+
+void check(hipError_t e, const char *what)
+{
+    if (e != hipSuccess)
+        die(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// util.cpp:3-8 — wall clock in microseconds
+double timestamp_us()
+{
+    struct timeval tv;
+    gettimeofday(&tv, nullptr);
+    return tv.tv_usec + tv.tv_sec * 1e6;
+}
+
+int device_count()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1)
+        die("no HIP device available (the MI355X path has no CPU fallback)");
+    return n;
+}
+
+int unit_device(int unit) { return unit % device_count(); }
+
+struct hw_matrix_impl {
+    csr_hw_matrix pub;  // must stay the first member: callers see a csr_hw_matrix*
+    spmv_plan *plan = nullptr;
+    int unit = 0, device = 0;
+    IndexType row_begin = 0, row_end = 0;
+    BusDataType *sub[1] = {nullptr};
+    IndexType nr_rows[1] = {0}, nr_cols[1] = {0}, nr_nzeros[1] = {0}, nr_ci[1] = {0}, nr_val[1] = {0};
+};
+
+struct hw_vector_impl {
+    csr_hw_vector pub;  // first member
+    BusDataType *vals[1] = {nullptr};
+    IndexType nr_values[1] = {0};
+    std::vector<ValueType *> per_device;  // x: a copy on every device in use; y: one buffer
+    int device = 0;
+};
+
+hw_matrix_impl *impl(csr_hw_matrix *m) { return reinterpret_cast<hw_matrix_impl *>(m); }
+hw_vector_impl *impl(csr_hw_vector *v) { return reinterpret_cast<hw_vector_impl *>(v); }
+
+std::mutex g_mu;
+int g_units_in_use = 0;                 // units of the most recent create_csr_hw_matrix
+std::vector<hipStream_t> g_streams;     // one stream per unit
+
+hipStream_t unit_stream(int unit)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_streams.size() <= unit)
+        g_streams.resize(unit + 1, nullptr);
+    if (!g_streams[unit]) {
+        check(hipSetDevice(unit_device(unit)), "hipSetDevice");
+        check(hipStreamCreateWithFlags(&g_streams[unit], hipStreamNonBlocking), "hipStreamCreate");
+    }
+    return g_streams[unit];
+}
+
+uint64_t ceil16(uint64_t bytes) { return (bytes + 15) / 16; }
+
+}  // namespace
+
+extern "C" {
+
+int spmv_hw_units(void)
+{
+    const char *s = std::getenv("SPMV_NGPUS");
+    int u = s ? std::atoi(s) : 1;
+    return u < 1 ? 1 : u;
+}
+
+// csr_hw_wrapper.cpp:3-80 (+ csr_hw.cpp:377-429 per CU count)
+void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool ***empty_rows_bitmap)
+{
+    if (!matrix || !hw_matrix || !empty_rows_bitmap)
+        die("create_csr_hw_matrix: null argument");
+    const int units = spmv_hw_units();
+    const IndexType n = matrix->nr_rows;
+    std::vector<IndexType> bounds(units + 1, 0);
+    if (spmv_partition_rows(matrix->row_ptr, n, units, bounds.data()))
+        die(spmv_hw_last_error());
+
+    *hw_matrix = (csr_hw_matrix **)std::malloc(units * sizeof(csr_hw_matrix *));
+    uint64_t in_bytes = 0, nnz_total = 0;
+    for (int u = 0; u < units; ++u) {
+        auto *h = new hw_matrix_impl();
+        h->unit = u;
+        h->device = unit_device(u);
+        h->row_begin = bounds[u];
+        h->row_end = bounds[u + 1];
+        if (spmv_plan_create_host(&h->plan, h->device, matrix, h->row_begin, h->row_end))
+            die(std::string("create_csr_hw_matrix: ") + spmv_hw_last_error());
+        spmv_plan_stats st;
+        spmv_plan_get_stats(h->plan, &st);
+        const uint64_t val_bytes = h->plan->nnz_pad * sizeof(ValueType);
+        h->sub[0] = reinterpret_cast<BusDataType *>(h->plan->d_col);
+        h->nr_rows[0] = (IndexType)st.nr_nonempty_rows;
+        h->nr_cols[0] = matrix->nr_cols;
+        h->nr_nzeros[0] = (IndexType)h->plan->nnz_pad;
+        h->nr_ci[0] = (IndexType)ceil16(st.device_bytes - val_bytes);
+        h->nr_val[0] = (IndexType)ceil16(val_bytes);
+        h->pub.submatrix = h->sub;
+        h->pub.nr_rows = h->nr_rows;
+        h->pub.nr_cols = h->nr_cols;
+        h->pub.nr_nzeros = h->nr_nzeros;
+        h->pub.nr_ci = h->nr_ci;
+        h->pub.nr_val = h->nr_val;
+        h->pub.blocks = 1;
+        (*hw_matrix)[u] = &h->pub;
+        in_bytes += st.device_bytes;
+        nnz_total += st.nr_nzeros;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_units_in_use = units;
+    }
+    // empty_rows_bitmap[block][row] (csr_hw.cpp:391-393, :340-347): inner rows live inside the
+    // outer allocation, so the caller's free(outer) (main.cpp:95) releases all of it.
+    const int blocks = 1;
+    bool **bm = (bool **)std::malloc(blocks * sizeof(bool *) + size_t(blocks) * n * sizeof(bool) + 1);
+    bool *rows = reinterpret_cast<bool *>(bm + blocks);
+    for (IndexType r = 0; r < n; ++r)
+        rows[r] = matrix->row_ptr[r + 1] == matrix->row_ptr[r];
+    bm[0] = rows;
+    *empty_rows_bitmap = bm;
+
+    // csr_hw.cpp:420-421
+    const double mb = 8.0 * 1024 * 1024;
+    const double in_mb = in_bytes * 8.0 / mb, out_mb = double(n) * VALUE_TYPE_BIT_WIDTH / mb;
+    std::cout << "Total non-zeros : " << nnz_total << ". Total " << in_mb + out_mb
+              << " MB transferred ( in : " << in_mb << ", out : " << out_mb << ")\n";
+}
+
+// csr_hw_wrapper.cpp:82-185: one y vector per unit (its row slice), on that unit's device
+void create_csr_hw_y_vector(csr_hw_matrix **hw_matrix, csr_hw_vector ***hw_vector)
+{
+    if (!hw_matrix || !hw_vector)
+        die("create_csr_hw_y_vector: null argument");
+    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    *hw_vector = (csr_hw_vector **)std::malloc(units * sizeof(csr_hw_vector *));
+    for (int u = 0; u < units; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        auto *v = new hw_vector_impl();
+        v->device = m->device;
+        const IndexType rows = m->row_end - m->row_begin;
+        ValueType *d = nullptr;
+        check(hipSetDevice(v->device), "hipSetDevice");
+        if (rows)
+            check(hipMalloc((void **)&d, size_t(rows) * sizeof(ValueType)), "hipMalloc(y)");
+        v->per_device.assign(1, d);
+        v->vals[0] = reinterpret_cast<BusDataType *>(d);
+        v->nr_values[0] = rows;
+        v->pub.values = v->vals;
+        v->pub.nr_values = v->nr_values;
+        v->pub.blocks = 1;
+        (*hw_vector)[u] = &v->pub;
+    }
+}
+
+// csr_hw_wrapper.cpp:187-191 (+ write_csr_hw_vector, csr_hw.cpp:1470-1488): x is uploaded
+// once to every device that hosts a unit.
+void create_csr_hw_x_vector(csr_hw_vector **hw_x, csr_vector *x, int blocks, IndexType *nr_cols)
+{
+    if (!hw_x || !x || !nr_cols)
+        die("create_csr_hw_x_vector: null argument");
+    if (blocks != 1)
+        die("create_csr_hw_x_vector: blocks must be hw_matrix[0]->blocks (1)");
+    if (x->nr_values > nr_cols[0])
+        die("create_csr_hw_x_vector: x is longer than the matrix has columns");
+    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    const int ndev = std::min(units, device_count());
+    auto *v = new hw_vector_impl();
+    v->per_device.assign(ndev, nullptr);
+    const size_t cols = nr_cols[0];
+    for (int d = 0; d < ndev; ++d) {
+        check(hipSetDevice(d), "hipSetDevice");
+        ValueType *p = nullptr;
+        check(hipMalloc((void **)&p, std::max<size_t>(cols, 1) * sizeof(ValueType)), "hipMalloc(x)");
+        check(hipMemset(p, 0, std::max<size_t>(cols, 1) * sizeof(ValueType)), "hipMemset(x)");
+        if (x->nr_values)
+            check(hipMemcpy(p, x->values, size_t(x->nr_values) * sizeof(ValueType), hipMemcpyHostToDevice),
+                  "hipMemcpy(x)");
+        v->per_device[d] = p;
+    }
+    v->vals[0] = reinterpret_cast<BusDataType *>(v->per_device[0]);
+    v->nr_values[0] = (IndexType)cols;
+    v->pub.values = v->vals;
+    v->pub.nr_values = v->nr_values;
+    v->pub.blocks = 1;
+    *hw_x = &v->pub;
+}
+
+// csr_hw_wrapper.cpp:193-288
+void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga, bool **empty_rows_bitmap)
+{
+    (void)empty_rows_bitmap;  // the device representation carries its own row map
+    if (!hw_matrix || !hw_x || !y_fpga)
+        die("spmv_hw: null argument");
+    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    hw_vector_impl *x = impl(hw_x);
+    csr_hw_vector **hw_y = nullptr;
+    create_csr_hw_y_vector(hw_matrix, &hw_y);
+
+    const double hw_s = timestamp_us();
+    for (int u = 0; u < units; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        if ((size_t)m->device >= x->per_device.size())
+            die("spmv_hw: x vector was not uploaded to device " + std::to_string(m->device));
+        if (spmv_plan_run(m->plan, x->per_device[m->device], impl(hw_y[u])->per_device[0], unit_stream(u)))
+            die(std::string("spmv_hw: ") + spmv_hw_last_error());
+    }
+    for (int u = 0; u < units; ++u) {
+        check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
+        check(hipStreamSynchronize(unit_stream(u)), "spmv kernels");
+    }
+    const double hw_exec = (timestamp_us() - hw_s) / 1000.0;
+    std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
+
+    const double ra_s = timestamp_us();
+    std::vector<ValueType> stage;
+    for (int u = 0; u < units; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        const IndexType rows = m->row_end - m->row_begin;
+        if (!rows)
+            continue;
+        if (m->row_end > y_fpga->nr_values)
+            die("spmv_hw: y_fpga is shorter than the matrix has rows");
+        stage.resize(rows);
+        check(hipSetDevice(m->device), "hipSetDevice");
+        check(hipMemcpy(stage.data(), impl(hw_y[u])->per_device[0], size_t(rows) * sizeof(ValueType),
+                        hipMemcpyDeviceToHost),
+              "hipMemcpy(y)");
+        ValueType *dst = y_fpga->values + m->row_begin;
+        for (IndexType i = 0; i < rows; ++i)
+            dst[i] += stage[i];
+    }
+    const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
+    std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
+    std::printf("Total time  : %.6f ms elapsed\n", hw_exec + ra_exec);
+    std::fflush(stdout);
+    delete_csr_hw_y_vector(hw_y);
+}
+
+// csr_hw_wrapper.cpp:291-296
+void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix)
+{
+    if (!hw_matrix)
+        return;
+    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    for (int u = 0; u < units; ++u) {
+        if (!hw_matrix[u])
+            continue;
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        spmv_plan_destroy(m->plan);
+        delete m;
+    }
+    std::free(hw_matrix);
+}
+
+static void delete_vector(csr_hw_vector *v)
+{
+    if (!v)
+        return;
+    hw_vector_impl *h = impl(v);
+    for (size_t d = 0; d < h->per_device.size(); ++d) {
+        if (h->per_device[d]) {
+            (void)hipSetDevice(h->per_device.size() == 1 ? h->device : (int)d);
+            (void)hipFree(h->per_device[d]);
+        }
+    }
+    delete h;
+}
+
+// csr_hw_wrapper.cpp:298-303
+void delete_csr_hw_y_vector(csr_hw_vector **hw_vector)
+{
+    if (!hw_vector)
+        return;
+    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    for (int u = 0; u < units; ++u)
+        delete_vector(hw_vector[u]);
+    std::free(hw_vector);
+}
+
+// csr_hw_wrapper.cpp:305-308
+void delete_csr_hw_x_vector(csr_hw_vector *hw_vector) { delete_vector(hw_vector); }
+
+// csr_hw.cpp:1401-1409: MB of one unit's representation (computed in 64 bits)
+ValueType storage_overhead(csr_hw_matrix *matrix)
+{
+    if (!matrix)
+        return 0;
+    uint64_t bits = uint64_t(matrix->blocks) * 5 * INDEX_TYPE_BIT_WIDTH;
+    for (int b = 0; b < matrix->blocks; ++b)
+        bits += (uint64_t(matrix->nr_ci[b]) + matrix->nr_val[b]) * BUS_BIT_WIDTH;
+    return (ValueType)(bits / (8.0 * 1024 * 1024));
+}
+
+// csr_hw.cpp:1571-1590
+int verification(IndexType nr_values, ValueType *sw_values, ValueType *hw_values, int verbose)
+{
+    const ValueType diff_thres = (ValueType)1e-5;
+    int status = 0;
+    IndexType err_cnt = 0;
+    for (IndexType i = 0; i < nr_values; ++i) {
+        const ValueType diff = std::fabs(sw_values[i] - hw_values[i]);
+        if (verbose == 2)
+            std::cout << std::setprecision(14) << i << " : y_gold = " << sw_values[i]
+                      << "\ty_hw = " << hw_values[i] << "\n";
+        if (diff >= diff_thres || diff != diff) {
+            status = 1;
+            ++err_cnt;
+            if (verbose == 1 || verbose == 2)
+                std::cout << std::setprecision(14) << "\tError occurs at " << i << " : y_gold = "
+                          << sw_values[i] << ", y_hw = " << hw_values[i]
+                          << ". Relative difference is " << std::fabs(diff / sw_values[i]) << "\n";
+        }
+    }
+    if (status)
+        std::cout << "Total errors : " << err_cnt << "\n";
+    std::cout.flush();
+    return status;
+}
+
+}  // extern "C"

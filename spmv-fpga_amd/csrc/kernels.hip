@@ -1,0 +1,255 @@
+// HIP kernels of the MI355X SpMV hot path (gfx950, wave64).
+//
+// Replaces the reference's per-column-block FPGA dataflow
+//   read_data_submatrix (spmv.cpp:6-34) -> stream_data_col_ind / stream_data_values
+//   (spmv.cpp:36-64) -> compute_results (spmv.cpp:66-104) -> write_back_results
+//   (spmv.cpp:106-120), and the host scatter accum_results (csr_hw.cpp:1531-1565),
+// with one flat, nnz-balanced pass over the matrix:
+//
+//   k_spmv_tiles: one wave per 512-entry tile. Coalesced 1-KiB dwordx4 wave loads of col/val
+//     (read_data_submatrix + stream_data_*), a register gather of x, lane-local products and a
+//     segmented inclusive scan across the 64 lanes keyed by the row-end bitmap
+//     (compute_results: the reference emits a row sum when the row-end bit of a group is set,
+//     spmv.cpp:99-102). Row sums are stored straight to y at their row (write_back_results +
+//     accum_results); a row that crosses a tile boundary leaves its partial sums in head/tail.
+//   k_fixup: one thread per tile completes every row that crossed a tile boundary, adding the
+//     partials in tile order (deterministic, no atomics).
+// Roofline: HBM-bound gather, no MFMA.
+#include "spmv_internal.hpp"
+
+namespace spmvhw {
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// 4 consecutive logical entries [kb + 4*lane, +4) of a wave step.
+__device__ __forceinline__ void load_vals(const double *__restrict__ val, uint64_t kb, int lane,
+                                          double (&v)[4])
+{
+    // fp64 pair-interleaved layout: dev[kb + j*128 + 2*lane + i] = logical[kb + 4*lane + 2*j + i]
+    const double2 a = *reinterpret_cast<const double2 *>(val + kb + 2 * lane);
+    const double2 b = *reinterpret_cast<const double2 *>(val + kb + 128 + 2 * lane);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+__device__ __forceinline__ void load_vals(const float *__restrict__ val, uint64_t kb, int lane,
+                                          float (&v)[4])
+{
+    const float4 a = *reinterpret_cast<const float4 *>(val + kb + 4 * lane);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+
+template <typename V>
+__device__ __forceinline__ void emit(V sum, uint32_t r, bool to_head, V *__restrict__ head,
+                                     uint64_t t, const uint32_t *__restrict__ row_id,
+                                     V *__restrict__ y)
+{
+    if (to_head)
+        head[t] = sum;
+    else
+        y[row_id ? row_id[r] : r] = sum;
+}
+
+template <typename V, int U>
+__global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
+    const uint32_t *__restrict__ col, const V *__restrict__ val, const uint32_t *__restrict__ rowend,
+    const uint32_t *__restrict__ tile_info, const uint32_t *__restrict__ row_id,
+    const V *__restrict__ x, V *__restrict__ y, V *__restrict__ head, V *__restrict__ tail,
+    uint8_t *__restrict__ tflags, uint64_t nnz, uint64_t ntiles)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t t = (uint64_t)blockIdx.x * (kBlockThreads / kWave) + (threadIdx.x >> 6);
+    if (t >= ntiles)
+        return;  // wave-uniform
+    const uint64_t k0 = t * (uint64_t)(U * kStep);
+
+    // ---- issue every streaming load of the tile first (memory-level parallelism) ----
+    uint32_t c[U][4];
+    V v[U][4];
+    uint32_t fl[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t kb = k0 + (uint64_t)u * kStep;
+        const uint4 cc = *reinterpret_cast<const uint4 *>(col + kb + 4 * lane);
+        c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
+        load_vals(val, kb, lane, v[u]);
+        fl[u] = (rowend[(kb >> 5) + (lane >> 3)] >> ((lane & 7) * 4)) & 0xFu;
+    }
+    V xv[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            xv[u][j] = x[c[u][j]];
+
+    const uint32_t info = tile_info[t];
+    uint32_t rowc = info >> 1;          // compact row of the tile's first entry
+    bool pending = (info & 1u) != 0;    // first row end of the tile closes a row begun earlier
+    bool any_end = false, last_is_end = false;
+    V carry = V(0);
+
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        V p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            p[j] = v[u][j] * xv[u][j];
+        const uint32_t f = fl[u];
+
+        // lane-local sum of the entries after the lane's last row end
+        V o = p[0];
+        o = (f & 1u) ? p[1] : o + p[1];
+        o = (f & 2u) ? p[2] : o + p[2];
+        o = (f & 4u) ? p[3] : o + p[3];
+        o = (f & 8u) ? V(0) : o;
+        int closed = f != 0u;
+
+        // segmented inclusive scan across the wave: (I,F) <- (I_prev,F_prev) (+) (I,F)
+        V I = o;
+        int F = closed;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const V In = __shfl_up(I, d, kWave);
+            const int Fn = __shfl_up(F, d, kWave);
+            if (lane >= d) {
+                I = F ? I : In + I;
+                F = F | Fn;
+            }
+        }
+        V ex = __shfl_up(I, 1, kWave);
+        int fx = __shfl_up(F, 1, kWave);
+        if (lane == 0) {
+            ex = V(0);
+            fx = 0;
+        }
+        if (!fx)
+            ex = carry + ex;
+
+        const uint64_t b0 = __ballot(f & 1u), b1 = __ballot(f & 2u);
+        const uint64_t b2 = __ballot(f & 4u), b3 = __ballot(f & 8u);
+        const uint64_t bany = b0 | b1 | b2 | b3;
+        uint32_t r = rowc + lanes_below(b0) + lanes_below(b1) + lanes_below(b2) + lanes_below(b3);
+        bool to_head = pending && bany != 0 && lane == (int)(__ffsll((unsigned long long)bany) - 1);
+
+        V run = ex;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            run = run + p[j];
+            if (f & (1u << j)) {
+                emit(run, r, to_head, head, t, row_id, y);
+                to_head = false;
+                ++r;
+                run = V(0);
+            }
+        }
+
+        const V I63 = __shfl(I, kWave - 1, kWave);
+        const int F63 = __shfl(F, kWave - 1, kWave);
+        carry = F63 ? I63 : carry + I63;
+        rowc += (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+        if (bany) {
+            pending = false;
+            any_end = true;
+        }
+        last_is_end = (b3 >> 63) & 1ull;
+    }
+
+    if (lane == 0) {
+        const bool has_tail = !last_is_end && (k0 + (uint64_t)(U * kStep) < nnz);
+        if (has_tail)
+            tail[t] = carry;
+        tflags[t] = (uint8_t)((has_tail ? kHasTail : 0) | (any_end ? kHasEnd : 0));
+    }
+}
+
+// Completes rows that cross tile boundaries: partials are added in tile order.
+template <typename V>
+__global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ tflags,
+                                               const V *__restrict__ head, const V *__restrict__ tail,
+                                               const uint32_t *__restrict__ tile_info,
+                                               const uint32_t *__restrict__ row_id, V *__restrict__ y,
+                                               uint64_t ntiles)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles)
+        return;
+    const uint8_t f = tflags[t];
+    if (!(f & kHasTail))
+        return;
+    if (!(f & kHasEnd) && t > 0 && (tflags[t - 1] & kHasTail))
+        return;  // a middle tile: the row began in an earlier tile
+    V acc = tail[t];
+    uint64_t j = t + 1;
+    while (j < ntiles && !(tflags[j] & kHasEnd)) {
+        acc = acc + tail[j];
+        ++j;
+    }
+    if (j >= ntiles)
+        return;  // unreachable for a well-formed plan (the last stored entry ends a row)
+    acc = acc + head[j];
+    const uint32_t r = tile_info[t + 1] >> 1;
+    y[row_id ? row_id[r] : r] = acc;
+}
+
+// Copies logical CSR col/val into the padded hw representation (fp64: pair-interleaved).
+template <typename V>
+__global__ void k_pack(const IndexType *__restrict__ col_src, const V *__restrict__ val_src,
+                       uint64_t nnz, uint64_t nnz_pad, uint32_t ncols, uint32_t *__restrict__ col,
+                       V *__restrict__ val, uint32_t *__restrict__ bad)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz_pad)
+        return;
+    const bool in = k < nnz;
+    uint32_t c = in ? col_src[k] : 0u;
+    if (c >= ncols) {  // never let an out-of-range index reach the gather
+        atomicOr(bad, 1u);
+        c = 0u;
+    }
+    col[k] = c;
+    uint64_t dst = k;
+    if (sizeof(V) == 8) {
+        const uint64_t base = k & ~(uint64_t)(kStep - 1);
+        const uint32_t w = (uint32_t)(k & (kStep - 1));
+        const uint32_t ln = w >> 2, e = w & 3u;
+        dst = base + (e >> 1) * 128u + 2u * ln + (e & 1u);
+    }
+    val[dst] = in ? val_src[k] : V(0);
+}
+
+hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+{
+    if (p.ntiles == 0)
+        return hipSuccess;
+    const uint64_t waves_per_block = kBlockThreads / kWave;
+    const uint64_t blocks = (p.ntiles + waves_per_block - 1) / waves_per_block;
+    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps>), dim3((unsigned)blocks),
+                       dim3(kBlockThreads), 0, s, p.d_col, p.d_val, p.d_rowend, p.d_tile_info,
+                       p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.d_tflags, p.nnz, p.ntiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s)
+{
+    if (p.ntiles < 2)
+        return hipSuccess;
+    const uint64_t blocks = (p.ntiles + 255) / 256;
+    hipLaunchKernelGGL((k_fixup<ValueType>), dim3((unsigned)blocks), dim3(256), 0, s, p.d_tflags,
+                       p.d_head, p.d_tail, p.d_tile_info, p.d_row_id, d_y, p.ntiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, uint64_t nnz,
+                       uint64_t nnz_pad, uint32_t ncols, uint32_t *d_col, ValueType *d_val,
+                       uint32_t *d_bad, hipStream_t s)
+{
+    if (nnz_pad == 0)
+        return hipSuccess;
+    const uint64_t blocks = (nnz_pad + 255) / 256;
+    hipLaunchKernelGGL((k_pack<ValueType>), dim3((unsigned)blocks), dim3(256), 0, s, d_col_src,
+                       d_val_src, nnz, nnz_pad, ncols, d_col, d_val, d_bad);
+    return hipGetLastError();
+}
+
+}  // namespace spmvhw

@@ -1,0 +1,338 @@
+// Host side of the MI355X hw representation: O(rows + nnz/32) metadata build, device
+// upload/pack, launch sequence, timing, nnz-balanced partitioning.
+//
+// Roles taken over from the reference's host format builder (csr_hw.cpp):
+//   scan_matrix (:7-146)                  -> one pass over row_ptr (no per-nnz block search)
+//   prepare_balanced_hw_matrix (:327-361) -> empty rows become the row_id map; the per-CU
+//                                            nnz balance is spmv_partition_rows (units)
+//   hw_matrix_alloc (:151-183)            -> hipMalloc of the plan buffers
+//   create_block_matrix +
+//   generate_balanced_hw_submatrix (:190-318) -> k_pack on the GPU (O(nnz), coalesced)
+#include <algorithm>
+#include <cstring>
+#include <memory>
+
+#include "spmv_internal.hpp"
+
+namespace spmvhw {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+const char *get_error() { return g_err.c_str(); }
+
+int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,
+                                 const IndexType *h_row_ptr, const IndexType *col_src,
+                                 const ValueType *val_src, bool src_on_device, hipStream_t s)
+{
+    *out = nullptr;
+    if (nr_rows > 0 && h_row_ptr[0] != 0) {
+        set_error("row_ptr must be rebased to 0");
+        return 1;
+    }
+    const uint64_t nnz = nr_rows ? h_row_ptr[nr_rows] : 0;
+    for (IndexType r = 0; r < nr_rows; ++r) {
+        if (h_row_ptr[r + 1] < h_row_ptr[r]) {
+            set_error("row_ptr is not non-decreasing at row " + std::to_string(r));
+            return 1;
+        }
+    }
+    if (nnz > 0 && nr_cols == 0) {
+        set_error("matrix has non-zeros but zero columns");
+        return 1;
+    }
+    SPMV_TRY(hipSetDevice(device));
+
+    std::unique_ptr<spmv_plan> p(new spmv_plan());
+    p->device = device;
+    p->nr_rows = nr_rows;
+    p->nr_cols = nr_cols;
+    p->nnz = nnz;
+    p->nnz_pad = (nnz + kTileNnz - 1) / kTileNnz * kTileNnz;
+    p->ntiles = p->nnz_pad / kTileNnz;
+
+    // ---- host metadata: row-end bitmap, non-empty row map, tile table ----
+    std::vector<uint32_t> rowend(p->nnz_pad / 32, 0u);
+    std::vector<uint32_t> row_id;
+    uint64_t nzr = 0;
+    for (IndexType r = 0; r < nr_rows; ++r)
+        if (h_row_ptr[r + 1] > h_row_ptr[r])
+            ++nzr;
+    p->nzr = nzr;
+    p->has_empty = nzr < nr_rows;
+    if (p->has_empty)
+        row_id.reserve(nzr);
+    for (IndexType r = 0; r < nr_rows; ++r) {
+        if (h_row_ptr[r + 1] > h_row_ptr[r]) {
+            const uint64_t e = h_row_ptr[r + 1] - 1ull;
+            rowend[e >> 5] |= 1u << (e & 31);
+            if (p->has_empty)
+                row_id.push_back(r);
+        }
+    }
+    std::vector<uint32_t> tile_info(p->ntiles + 1, 0u);
+    {
+        uint64_t rr = 0, c = 0;
+        for (uint64_t t = 0; t <= p->ntiles; ++t) {
+            const uint64_t k = t * kTileNnz;
+            while (rr < nr_rows && h_row_ptr[rr + 1] <= k) {
+                if (h_row_ptr[rr + 1] > h_row_ptr[rr])
+                    ++c;
+                ++rr;
+            }
+            if (c > 0x7FFFFFFFull) {
+                set_error("too many non-empty rows for the tile table");
+                return 1;
+            }
+            const bool cont = k > 0 && k < nnz && !((rowend[(k - 1) >> 5] >> ((k - 1) & 31)) & 1u);
+            tile_info[t] = (uint32_t)(c << 1) | (cont ? 1u : 0u);
+        }
+    }
+
+    // ---- device buffers ----
+    auto alloc = [&](void **ptr, size_t bytes) -> hipError_t {
+        *ptr = nullptr;
+        return bytes ? hipMalloc(ptr, bytes) : hipSuccess;
+    };
+    SPMV_TRY(alloc((void **)&p->d_col, p->nnz_pad * sizeof(uint32_t)));
+    SPMV_TRY(alloc((void **)&p->d_val, p->nnz_pad * sizeof(ValueType)));
+    SPMV_TRY(alloc((void **)&p->d_rowend, rowend.size() * sizeof(uint32_t)));
+    SPMV_TRY(alloc((void **)&p->d_tile_info, tile_info.size() * sizeof(uint32_t)));
+    SPMV_TRY(alloc((void **)&p->d_head, p->ntiles * sizeof(ValueType)));
+    SPMV_TRY(alloc((void **)&p->d_tail, p->ntiles * sizeof(ValueType)));
+    SPMV_TRY(alloc((void **)&p->d_tflags, p->ntiles));
+    if (p->has_empty)
+        SPMV_TRY(alloc((void **)&p->d_row_id, row_id.size() * sizeof(uint32_t)));
+
+    if (!rowend.empty())
+        SPMV_TRY(hipMemcpyAsync(p->d_rowend, rowend.data(), rowend.size() * 4, hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipMemcpyAsync(p->d_tile_info, tile_info.data(), tile_info.size() * 4, hipMemcpyHostToDevice, s));
+    if (p->has_empty && !row_id.empty())
+        SPMV_TRY(hipMemcpyAsync(p->d_row_id, row_id.data(), row_id.size() * 4, hipMemcpyHostToDevice, s));
+
+    if (p->nnz_pad) {
+        uint32_t *d_bad = nullptr;
+        SPMV_TRY(hipMalloc((void **)&d_bad, sizeof(uint32_t)));
+        SPMV_TRY(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s));
+        if (src_on_device) {
+            SPMV_TRY(launch_pack(col_src, val_src, nnz, p->nnz_pad, nr_cols, p->d_col, p->d_val, d_bad, s));
+        } else {
+            IndexType *d_cs = nullptr;
+            ValueType *d_vs = nullptr;
+            SPMV_TRY(alloc((void **)&d_cs, nnz * sizeof(IndexType)));
+            SPMV_TRY(alloc((void **)&d_vs, nnz * sizeof(ValueType)));
+            if (nnz) {
+                SPMV_TRY(hipMemcpyAsync(d_cs, col_src, nnz * sizeof(IndexType), hipMemcpyHostToDevice, s));
+                SPMV_TRY(hipMemcpyAsync(d_vs, val_src, nnz * sizeof(ValueType), hipMemcpyHostToDevice, s));
+            }
+            SPMV_TRY(launch_pack(d_cs, d_vs, nnz, p->nnz_pad, nr_cols, p->d_col, p->d_val, d_bad, s));
+            SPMV_TRY(hipStreamSynchronize(s));
+            SPMV_TRY(hipFree(d_cs));
+            SPMV_TRY(hipFree(d_vs));
+        }
+        uint32_t bad = 0;
+        SPMV_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, s));
+        SPMV_TRY(hipStreamSynchronize(s));
+        SPMV_TRY(hipFree(d_bad));
+        if (bad) {
+            set_error("column index out of range (>= nr_cols)");
+            return 1;
+        }
+    }
+    SPMV_TRY(hipStreamSynchronize(s));
+    *out = p.release();
+    return 0;
+}
+
+}  // namespace spmvhw
+
+using namespace spmvhw;
+
+spmv_plan::~spmv_plan()
+{
+    (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
+    for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
+                      (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_tflags})
+        if (ptr)
+            (void)hipFree(ptr);
+    for (hipEvent_t e : ev)
+        (void)hipEventDestroy(e);
+}
+
+uint64_t spmv_plan::device_bytes() const
+{
+    return nnz_pad * (sizeof(uint32_t) + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
+           (has_empty ? nzr * 4 : 0) + ntiles * (2 * sizeof(ValueType) + 1);
+}
+
+// z*(sizeof(val)+4) + (n+1)*4 + m*sizeof(val) + n*sizeof(val)
+uint64_t spmv_plan::algorithmic_bytes() const
+{
+    return nnz * (sizeof(ValueType) + 4) + (uint64_t(nr_rows) + 1) * 4 +
+           uint64_t(nr_cols) * sizeof(ValueType) + uint64_t(nr_rows) * sizeof(ValueType);
+}
+
+extern "C" {
+
+const char *spmv_hw_last_error(void) { return get_error(); }
+int spmv_hw_value_bytes(void) { return (int)sizeof(ValueType); }
+
+int spmv_plan_create_device(spmv_plan **plan, int device, IndexType nr_rows, IndexType nr_cols,
+                            IndexType nr_nzeros, const IndexType *d_row_ptr,
+                            const IndexType *d_col_ind, const ValueType *d_values, void *stream)
+{
+    if (!plan || (nr_rows && !d_row_ptr)) {
+        set_error("spmv_plan_create_device: null argument");
+        return 1;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    SPMV_TRY(hipSetDevice(device));
+    std::vector<IndexType> rp(size_t(nr_rows) + 1, 0u);
+    if (nr_rows) {
+        SPMV_TRY(hipMemcpyAsync(rp.data(), d_row_ptr, rp.size() * sizeof(IndexType), hipMemcpyDeviceToHost, s));
+        SPMV_TRY(hipStreamSynchronize(s));
+    }
+    const IndexType base = rp[0];
+    for (auto &e : rp)
+        e -= base;
+    if (rp[nr_rows] != nr_nzeros) {
+        set_error("spmv_plan_create_device: row_ptr[n]-row_ptr[0] != nr_nzeros");
+        return 1;
+    }
+    return plan_create_from_host_rowptr(plan, device, nr_rows, nr_cols, rp.data(),
+                                        d_col_ind ? d_col_ind + base : nullptr,
+                                        d_values ? d_values + base : nullptr, true, s);
+}
+
+int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *m, IndexType row_begin,
+                          IndexType row_end)
+{
+    if (!plan || !m || row_begin > row_end || row_end > m->nr_rows) {
+        set_error("spmv_plan_create_host: bad arguments");
+        return 1;
+    }
+    const IndexType n = row_end - row_begin;
+    const IndexType base = m->row_ptr[row_begin];
+    std::vector<IndexType> rp(size_t(n) + 1);
+    for (IndexType r = 0; r <= n; ++r)
+        rp[r] = m->row_ptr[row_begin + r] - base;
+    hipStream_t s = nullptr;
+    return plan_create_from_host_rowptr(plan, device, n, m->nr_cols, rp.data(), m->col_ind + base,
+                                        m->values + base, false, s);
+}
+
+int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, void *stream)
+{
+    if (!cp) {
+        set_error("spmv_plan_run: null plan");
+        return 1;
+    }
+    spmv_plan *p = const_cast<spmv_plan *>(cp);
+    hipStream_t s = (hipStream_t)stream;
+    SPMV_TRY(hipSetDevice(p->device));
+    if (p->nr_rows == 0)
+        return 0;
+    if (p->has_empty || p->nnz == 0)
+        SPMV_TRY(hipMemsetAsync(d_y, 0, size_t(p->nr_rows) * sizeof(ValueType), s));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (p->timing) {
+        if (p->ev_used + 2 > p->ev.size()) {
+            for (int i = 0; i < 2; ++i) {
+                hipEvent_t e;
+                SPMV_TRY(hipEventCreate(&e));
+                p->ev.push_back(e);
+            }
+        }
+        e0 = p->ev[p->ev_used];
+        e1 = p->ev[p->ev_used + 1];
+        p->ev_used += 2;
+        SPMV_TRY(hipEventRecord(e0, s));
+    }
+    SPMV_TRY(launch_spmv(*p, d_x, d_y, s));
+    if (p->timing)
+        SPMV_TRY(hipEventRecord(e1, s));
+    SPMV_TRY(launch_fixup(*p, d_y, s));
+    return 0;
+}
+
+int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
+{
+    if (!p || !st) {
+        set_error("spmv_plan_get_stats: null argument");
+        return 1;
+    }
+    std::memset(st, 0, sizeof(*st));
+    st->nr_rows = p->nr_rows;
+    st->nr_cols = p->nr_cols;
+    st->nr_nzeros = p->nnz;
+    st->nr_nonempty_rows = p->nzr;
+    st->nr_tiles = p->ntiles;
+    st->tile_nnz = kTileNnz;
+    st->device_bytes = p->device_bytes();
+    st->algorithmic_bytes = p->algorithmic_bytes();
+    st->device = p->device;
+    st->kernel = p->kernel;
+    st->blocks = 1;
+    st->lds_tiles_pct = 0;
+    return 0;
+}
+
+int spmv_plan_set_timing(spmv_plan *p, int enable)
+{
+    if (!p) {
+        set_error("spmv_plan_set_timing: null plan");
+        return 1;
+    }
+    p->timing = enable != 0;
+    p->ev_used = 0;
+    return 0;
+}
+
+int spmv_plan_get_timing(spmv_plan *p, double *mean_ms, double *total_ms, int *launches)
+{
+    if (!p) {
+        set_error("spmv_plan_get_timing: null plan");
+        return 1;
+    }
+    SPMV_TRY(hipSetDevice(p->device));
+    double tot = 0.0;
+    int n = 0;
+    for (size_t i = 0; i + 1 < p->ev_used; i += 2) {
+        SPMV_TRY(hipEventSynchronize(p->ev[i + 1]));
+        float ms = 0.f;
+        SPMV_TRY(hipEventElapsedTime(&ms, p->ev[i], p->ev[i + 1]));
+        tot += ms;
+        ++n;
+    }
+    p->ev_used = 0;
+    if (mean_ms)
+        *mean_ms = n ? tot / n : 0.0;
+    if (total_ms)
+        *total_ms = tot;
+    if (launches)
+        *launches = n;
+    return 0;
+}
+
+void spmv_plan_destroy(spmv_plan *p) { delete p; }
+
+int spmv_partition_rows(const IndexType *row_ptr, IndexType nr_rows, int units, IndexType *bounds)
+{
+    if (!row_ptr || !bounds || units < 1) {
+        set_error("spmv_partition_rows: bad arguments");
+        return 1;
+    }
+    const uint64_t nnz = uint64_t(row_ptr[nr_rows]) - row_ptr[0];
+    bounds[0] = 0;
+    for (int u = 1; u < units; ++u) {
+        const uint64_t target = row_ptr[0] + nnz * uint64_t(u) / uint64_t(units);
+        // first row whose start is >= target
+        const IndexType *it = std::lower_bound(row_ptr, row_ptr + nr_rows, (IndexType)target);
+        IndexType b = (IndexType)(it - row_ptr);
+        bounds[u] = std::max(b, bounds[u - 1]);
+    }
+    bounds[units] = nr_rows;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// Internal declarations of libspmv_hw (not part of the C-ABI).
+//
+// The MI355X hw representation of one unit's row slice ("plan"), DESIGN.md §3:
+//   col      u32[nnz_pad]   column index of every stored non-zero, CSR order
+//   val      V[nnz_pad]     values; fp64 is pair-interleaved inside each 256-entry wave step so
+//                           that every lane's 4 consecutive entries arrive by two fully coalesced
+//                           1-KiB dwordx4 wave loads (fp32 keeps CSR order: one dwordx4)
+//   rowend   u32[nnz_pad/32] bit k set <=> entry k is the last entry of its row. This is the
+//                           reference's "last element of row" flag (csr_hw.cpp:288-292, bit 15 of
+//                           each 16-bit column field) moved to a bitmap: 1 bit/nnz instead of 16.
+//   tile_info u32[ntiles+1]  (compact row index of the tile's first entry << 1) | (1 if that
+//                           entry continues a row begun in an earlier tile)
+//   row_id   u32[nzr]       slice row of each non-empty row; absent when no row is empty. This
+//                           replaces the reference's empty_rows_bitmap scatter
+//                           (csr_hw.cpp:1531-1565) with an index map.
+// Entries past nnz (padding to a whole tile) have col 0, value 0 and no row-end bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "csr_hw_wrapper.h"
+
+namespace spmvhw {
+
+constexpr int kWave = 64;
+constexpr int kLaneEntries = 4;                    // entries per lane per wave step
+constexpr int kStep = kWave * kLaneEntries;        // 256 entries per wave step
+constexpr int kTileSteps = 2;                      // wave steps per tile
+constexpr int kTileNnz = kStep * kTileSteps;       // 512 entries per wave tile
+constexpr int kBlockThreads = 256;                 // 4 waves = 4 tiles per workgroup
+
+// tile flags written by the main kernel, read by the fix-up kernel
+constexpr uint8_t kHasTail = 1;   // tile ends inside a row that continues in the next tile
+constexpr uint8_t kHasEnd = 2;    // tile contains at least one row end
+}  // namespace spmvhw
+
+struct spmv_plan {
+    int device = 0;
+    IndexType nr_rows = 0, nr_cols = 0;
+    uint64_t nnz = 0, nnz_pad = 0;
+    uint64_t nzr = 0;          // non-empty rows
+    uint64_t ntiles = 0;
+    bool has_empty = false;
+    int kernel = 0;
+
+    uint32_t *d_col = nullptr;
+    ValueType *d_val = nullptr;
+    uint32_t *d_rowend = nullptr;
+    uint32_t *d_tile_info = nullptr;
+    uint32_t *d_row_id = nullptr;
+    ValueType *d_head = nullptr;
+    ValueType *d_tail = nullptr;
+    uint8_t *d_tflags = nullptr;
+
+    // timing (HIP events around the main kernel, on the launch stream)
+    bool timing = false;
+    std::vector<hipEvent_t> ev;   // pairs
+    size_t ev_used = 0;
+
+    uint64_t device_bytes() const;
+    uint64_t algorithmic_bytes() const;
+    ~spmv_plan();  // frees every device buffer and event (also on error paths)
+};
+
+namespace spmvhw {
+
+void set_error(const std::string &msg);
+const char *get_error();
+
+// kernels.hip
+hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);
+hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s);
+hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, uint64_t nnz,
+                       uint64_t nnz_pad, uint32_t ncols, uint32_t *d_col, ValueType *d_val,
+                       uint32_t *d_bad, hipStream_t s);
+
+// plan.cpp helpers shared with the wrapper
+int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,
+                                 const IndexType *h_row_ptr /* rebased, nr_rows+1 */,
+                                 const IndexType *col_src, const ValueType *val_src,
+                                 bool src_on_device, hipStream_t s);
+}  // namespace spmvhw
+
+#define SPMV_TRY(expr)                                                                        \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            spmvhw::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));             \
+            return 1;                                                                         \
+        }                                                                                     \
+    } while (0)

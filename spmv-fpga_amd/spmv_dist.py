@@ -1,0 +1,60 @@
+"""Multi-GPU layout of the SpMV path: one process per GPU, torch.distributed over RCCL/xGMI.
+
+The reference's only parallelism is ComputeUnits pipelines that each own a contiguous,
+nnz-balanced row slice of every column block (csr_hw.cpp:459-468) with x replicated into every
+CU (spmv.cpp:280-294); the host then merges the per-CU y (accum_results, csr_hw.cpp:1531-1565,
+loop csr_hw_wrapper.cpp:276-281). Here a CU is a GPU rank:
+
+  * row_slice(): the nnz-balanced contiguous slice of rank r (spmv_partition_rows in the C-ABI,
+    S1 rule without the FPGA alignment rules S2/S3);
+  * x is generated/uploaded on every rank (replicated, no collective);
+  * the y merge is a real exchange step, done two ways over RCCL:
+      - "reduce": every rank contributes a full-length partial y (zeros outside its slice) to
+        an RCCL reduce(SUM) on rank 0 -- the literal accum_results '+=' mapping;
+      - "gather": ranks send only their disjoint slices to rank 0 (bandwidth-optimal).
+Both return the full y on rank 0 and None elsewhere.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def row_slice(bounds, rank: int):
+    return int(bounds[rank]), int(bounds[rank + 1])
+
+
+def exchange_reduce(y_slice: torch.Tensor, row_begin: int, n_rows: int, dst: int = 0):
+    """accum_results semantics: full-length partials summed into rank `dst`."""
+    full = torch.zeros(n_rows, dtype=y_slice.dtype, device=y_slice.device)
+    full[row_begin:row_begin + y_slice.numel()] = y_slice
+    dist.reduce(full, dst=dst, op=dist.ReduceOp.SUM)
+    return full if dist.get_rank() == dst else None
+
+
+def exchange_gather(y_slice: torch.Tensor, counts, dst: int = 0):
+    """Disjoint slices to rank `dst` (each rank sends only its own rows)."""
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    maxc = int(max(counts))
+    buf = torch.zeros(maxc, dtype=y_slice.dtype, device=y_slice.device)
+    buf[:y_slice.numel()] = y_slice
+    if rank == dst:
+        parts = [torch.empty(maxc, dtype=y_slice.dtype, device=y_slice.device) for _ in range(world)]
+        dist.gather(buf, gather_list=parts, dst=dst)
+        return torch.cat([parts[r][:int(counts[r])] for r in range(world)])
+    dist.gather(buf, dst=dst)
+    return None
+
+
+def max_over_ranks(value: float, device) -> float:
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def slice_counts(bounds) -> np.ndarray:
+    b = np.asarray(bounds, np.int64)
+    return np.diff(b)

@@ -1,0 +1,352 @@
+"""Python host mirror of the csr_hw_wrapper drop-in boundary (ctypes over libspmv_hw_*.so).
+
+The C-ABI (include/csr_hw_wrapper.h) is the product boundary; this module binds it with the
+reference's names and argument meaning (euroexa/spmv-fpga src/csr_hw_wrapper.h:9-17,
+src/csr_hw.h:140,148) so tests and the bench read like the reference's main.cpp:46-97 flow.
+It has no compute of its own and no fallback: if the HIP library is not built, every entry
+point raises.
+
+Two precisions, as the reference's DOUBLE build knob (util.h:18-26): dtype=np.float64 binds
+libspmv_hw_f64.so, dtype=np.float32 binds libspmv_hw_f32.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+try:  # share torch's HIP runtime when torch is present (it must be loaded first)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the pure C-ABI path
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "lib")
+_LIBS: dict = {}
+
+IndexType = ctypes.c_uint32
+
+
+def lib_path(dtype=np.float64) -> str:
+    name = {8: "libspmv_hw_f64.so", 4: "libspmv_hw_f32.so"}[np.dtype(dtype).itemsize]
+    return os.path.join(LIBDIR, name)
+
+
+def build() -> None:
+    """Compile both precisions for gfx950 (hipcc, see Makefile)."""
+    subprocess.run(["make", "-s", "-C", HERE, "-j2"], check=True)
+
+
+def _value_ctype(dtype):
+    return ctypes.c_double if np.dtype(dtype) == np.float64 else ctypes.c_float
+
+
+class BusDataType(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
+def _structs(dtype):
+    V = _value_ctype(dtype)
+
+    class csr_matrix(ctypes.Structure):  # csr.h:15-24
+        _fields_ = [("row_ptr", ctypes.POINTER(IndexType)), ("col_ind", ctypes.POINTER(IndexType)),
+                    ("values", ctypes.POINTER(V)), ("nr_nzeros", IndexType), ("nr_rows", IndexType),
+                    ("nr_cols", IndexType), ("Filename", ctypes.c_char_p)]
+
+    class csr_vector(ctypes.Structure):  # csr.h:26-29
+        _fields_ = [("values", ctypes.POINTER(V)), ("nr_values", IndexType)]
+
+    class csr_hw_matrix(ctypes.Structure):  # csr_hw.h:16-26
+        _fields_ = [("submatrix", ctypes.POINTER(ctypes.POINTER(BusDataType))),
+                    ("nr_rows", ctypes.POINTER(IndexType)), ("nr_cols", ctypes.POINTER(IndexType)),
+                    ("nr_nzeros", ctypes.POINTER(IndexType)), ("nr_ci", ctypes.POINTER(IndexType)),
+                    ("nr_val", ctypes.POINTER(IndexType)), ("blocks", ctypes.c_int)]
+
+    class csr_hw_vector(ctypes.Structure):  # csr_hw.h:28-33
+        _fields_ = [("values", ctypes.POINTER(ctypes.POINTER(BusDataType))),
+                    ("nr_values", ctypes.POINTER(IndexType)), ("blocks", ctypes.c_int)]
+
+    return csr_matrix, csr_vector, csr_hw_matrix, csr_hw_vector
+
+
+class spmv_plan_stats(ctypes.Structure):
+    _fields_ = [("nr_rows", ctypes.c_uint64), ("nr_cols", ctypes.c_uint64),
+                ("nr_nzeros", ctypes.c_uint64), ("nr_nonempty_rows", ctypes.c_uint64),
+                ("nr_tiles", ctypes.c_uint64), ("tile_nnz", ctypes.c_uint64),
+                ("device_bytes", ctypes.c_uint64), ("algorithmic_bytes", ctypes.c_uint64),
+                ("device", ctypes.c_int32), ("kernel", ctypes.c_int32), ("blocks", ctypes.c_int32),
+                ("lds_tiles_pct", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every symbol include/csr_hw_wrapper.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "create_csr_hw_matrix", "create_csr_hw_y_vector", "create_csr_hw_x_vector", "spmv_hw",
+    "delete_csr_hw_matrix", "delete_csr_hw_y_vector", "delete_csr_hw_x_vector",
+    "storage_overhead", "verification",
+    "spmv_hw_units", "spmv_hw_value_bytes", "spmv_hw_last_error",
+    "spmv_plan_create_device", "spmv_plan_create_host", "spmv_plan_run", "spmv_plan_get_stats",
+    "spmv_plan_set_timing", "spmv_plan_get_timing", "spmv_plan_destroy", "spmv_partition_rows",
+    "spmv_gen_banded", "spmv_gen_powerlaw_row_ptr", "spmv_gen_fill", "spmv_gen_vector",
+]
+
+
+class Lib:
+    """Typed handle on one precision of libspmv_hw."""
+
+    def __init__(self, dtype=np.float64):
+        self.dtype = np.dtype(dtype)
+        path = lib_path(self.dtype)
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is not built (run `make -C spmv-fpga_amd`); "
+                               "the MI355X path has no CPU fallback")
+        self.L = L = ctypes.CDLL(path)
+        self.V = V = _value_ctype(self.dtype)
+        (self.csr_matrix, self.csr_vector, self.csr_hw_matrix, self.csr_hw_vector) = _structs(self.dtype)
+        PM = ctypes.POINTER(self.csr_hw_matrix)
+        PV = ctypes.POINTER(self.csr_hw_vector)
+        PB = ctypes.POINTER(ctypes.POINTER(ctypes.c_bool))
+        vp, up = ctypes.c_void_p, ctypes.POINTER(IndexType)
+        sig = {
+            "create_csr_hw_matrix": (None, [ctypes.POINTER(self.csr_matrix), ctypes.POINTER(ctypes.POINTER(PM)),
+                                            ctypes.POINTER(PB)]),
+            "create_csr_hw_y_vector": (None, [ctypes.POINTER(PM), ctypes.POINTER(ctypes.POINTER(PV))]),
+            "create_csr_hw_x_vector": (None, [ctypes.POINTER(PV), ctypes.POINTER(self.csr_vector), ctypes.c_int, up]),
+            "spmv_hw": (None, [ctypes.POINTER(PM), PV, ctypes.POINTER(self.csr_vector), PB]),
+            "delete_csr_hw_matrix": (None, [ctypes.POINTER(PM)]),
+            "delete_csr_hw_y_vector": (None, [ctypes.POINTER(PV)]),
+            "delete_csr_hw_x_vector": (None, [PV]),
+            "storage_overhead": (V, [PM]),
+            "verification": (ctypes.c_int, [IndexType, ctypes.POINTER(V), ctypes.POINTER(V), ctypes.c_int]),
+            "spmv_hw_units": (ctypes.c_int, []),
+            "spmv_hw_value_bytes": (ctypes.c_int, []),
+            "spmv_hw_last_error": (ctypes.c_char_p, []),
+            "spmv_plan_create_device": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, IndexType, IndexType,
+                                                       IndexType, vp, vp, vp, vp]),
+            "spmv_plan_create_host": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int,
+                                                     ctypes.POINTER(self.csr_matrix), IndexType, IndexType]),
+            "spmv_plan_run": (ctypes.c_int, [vp, vp, vp, vp]),
+            "spmv_plan_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(spmv_plan_stats)]),
+            "spmv_plan_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+            "spmv_plan_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+            "spmv_plan_destroy": (None, [vp]),
+            "spmv_partition_rows": (ctypes.c_int, [up, IndexType, ctypes.c_int, up]),
+            "spmv_gen_banded": (ctypes.c_int, [IndexType, IndexType, ctypes.c_uint64, vp, vp, vp, vp]),
+            "spmv_gen_powerlaw_row_ptr": (ctypes.c_int, [IndexType, ctypes.c_uint64, IndexType, ctypes.c_uint64,
+                                                         up, ctypes.POINTER(ctypes.c_double)]),
+            "spmv_gen_fill": (ctypes.c_int, [IndexType, IndexType, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp, vp]),
+            "spmv_gen_vector": (ctypes.c_int, [IndexType, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
+                                               ctypes.c_double, vp, vp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.spmv_hw_value_bytes() != self.dtype.itemsize:
+            raise RuntimeError(f"{path} was built for a different precision")
+        self._libc = ctypes.CDLL(None)
+        self._libc.free.argtypes = [ctypes.c_void_p]
+
+    # ---- error helper for Part-2 calls ----
+    def _ok(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.L.spmv_hw_last_error().decode()}")
+
+    # ---- host-side helpers ----
+    def make_csr_matrix(self, row_ptr, col, val, nr_cols: int):
+        """A csr_matrix (csr.h:15-24) viewing numpy arrays (kept alive on the struct)."""
+        row_ptr = np.ascontiguousarray(row_ptr, np.uint32)
+        col = np.ascontiguousarray(col, np.uint32)
+        val = np.ascontiguousarray(val, self.dtype)
+        m = self.csr_matrix()
+        m.row_ptr = row_ptr.ctypes.data_as(ctypes.POINTER(IndexType))
+        m.col_ind = col.ctypes.data_as(ctypes.POINTER(IndexType))
+        m.values = val.ctypes.data_as(ctypes.POINTER(self.V))
+        m.nr_nzeros = int(row_ptr[-1])
+        m.nr_rows = len(row_ptr) - 1
+        m.nr_cols = int(nr_cols)
+        m.Filename = None
+        m._keep = (row_ptr, col, val)
+        return m
+
+    def make_csr_vector(self, values):
+        values = np.ascontiguousarray(values, self.dtype)
+        v = self.csr_vector()
+        v.values = values.ctypes.data_as(ctypes.POINTER(self.V))
+        v.nr_values = len(values)
+        v._keep = values
+        return v
+
+    # ---- Part 1: reference API (same names; failures exit the process like the C-ABI) ----
+    def create_csr_hw_matrix(self, matrix):
+        hw = ctypes.POINTER(ctypes.POINTER(self.csr_hw_matrix))()
+        bm = ctypes.POINTER(ctypes.POINTER(ctypes.c_bool))()
+        self.L.create_csr_hw_matrix(ctypes.byref(matrix), ctypes.byref(hw), ctypes.byref(bm))
+        return hw, bm
+
+    def create_csr_hw_x_vector(self, x_vec, blocks: int, nr_cols):
+        hx = ctypes.POINTER(self.csr_hw_vector)()
+        self.L.create_csr_hw_x_vector(ctypes.byref(hx), ctypes.byref(x_vec), blocks, nr_cols)
+        return hx
+
+    def create_csr_hw_y_vector(self, hw_matrix):
+        hy = ctypes.POINTER(ctypes.POINTER(self.csr_hw_vector))()
+        self.L.create_csr_hw_y_vector(hw_matrix, ctypes.byref(hy))
+        return hy
+
+    def spmv_hw(self, hw_matrix, hw_x, y_vec, bitmap) -> None:
+        self.L.spmv_hw(hw_matrix, hw_x, ctypes.byref(y_vec), bitmap)
+
+    def delete_csr_hw_matrix(self, hw_matrix) -> None:
+        self.L.delete_csr_hw_matrix(hw_matrix)
+
+    def delete_csr_hw_y_vector(self, hw_y) -> None:
+        self.L.delete_csr_hw_y_vector(hw_y)
+
+    def delete_csr_hw_x_vector(self, hw_x) -> None:
+        self.L.delete_csr_hw_x_vector(hw_x)
+
+    def free_bitmap(self, bitmap) -> None:
+        """main.cpp:95 frees only the outer array; that releases the whole bitmap here."""
+        self._libc.free(ctypes.cast(bitmap, ctypes.c_void_p))
+
+    def storage_overhead(self, hw_matrix_unit) -> float:
+        return float(self.L.storage_overhead(hw_matrix_unit))
+
+    def verification(self, sw, hw, verbose: int = 0) -> int:
+        sw = np.ascontiguousarray(sw, self.dtype)
+        hw = np.ascontiguousarray(hw, self.dtype)
+        return int(self.L.verification(len(sw), sw.ctypes.data_as(ctypes.POINTER(self.V)),
+                                       hw.ctypes.data_as(ctypes.POINTER(self.V)), verbose))
+
+    def units(self) -> int:
+        return int(self.L.spmv_hw_units())
+
+    def partition_rows(self, row_ptr, units: int):
+        row_ptr = np.ascontiguousarray(row_ptr, np.uint32)
+        bounds = np.zeros(units + 1, np.uint32)
+        self._ok(self.L.spmv_partition_rows(row_ptr.ctypes.data_as(ctypes.POINTER(IndexType)),
+                                            len(row_ptr) - 1, units,
+                                            bounds.ctypes.data_as(ctypes.POINTER(IndexType))),
+                 "spmv_partition_rows")
+        return bounds
+
+    def powerlaw_row_ptr(self, n: int, nnz: int, max_len: int = 65536, seed: int = 4):
+        rp = np.zeros(n + 1, np.uint32)
+        s = ctypes.c_double()
+        self._ok(self.L.spmv_gen_powerlaw_row_ptr(n, nnz, max_len, seed,
+                                                  rp.ctypes.data_as(ctypes.POINTER(IndexType)),
+                                                  ctypes.byref(s)), "spmv_gen_powerlaw_row_ptr")
+        return rp, s.value
+
+
+class Plan:
+    """One unit's device-resident matrix slice (include/csr_hw_wrapper.h Part 2)."""
+
+    def __init__(self, lib: Lib, handle: ctypes.c_void_p):
+        self.lib = lib
+        self.h = handle
+
+    @classmethod
+    def from_device(cls, lib: Lib, row_ptr, col, val, nr_cols: int, device: int = 0, stream=None):
+        """row_ptr/col/val: torch tensors on `device` (uint32 viewed as int32, values of lib.dtype)."""
+        h = ctypes.c_void_p()
+        n = row_ptr.numel() - 1
+        nnz = int(row_ptr[-1].item()) - int(row_ptr[0].item()) if n >= 0 else 0
+        lib._ok(lib.L.spmv_plan_create_device(ctypes.byref(h), device, n, nr_cols, nnz & 0xFFFFFFFF,
+                                              row_ptr.data_ptr(), col.data_ptr(), val.data_ptr(),
+                                              _stream_ptr(stream)), "spmv_plan_create_device")
+        return cls(lib, h)
+
+    @classmethod
+    def from_host(cls, lib: Lib, matrix, row_begin: int, row_end: int, device: int = 0):
+        h = ctypes.c_void_p()
+        lib._ok(lib.L.spmv_plan_create_host(ctypes.byref(h), device, ctypes.byref(matrix), row_begin, row_end),
+                "spmv_plan_create_host")
+        return cls(lib, h)
+
+    def run(self, x, y, stream=None) -> None:
+        self.lib._ok(self.lib.L.spmv_plan_run(self.h, x.data_ptr(), y.data_ptr(), _stream_ptr(stream)),
+                     "spmv_plan_run")
+
+    def stats(self) -> dict:
+        st = spmv_plan_stats()
+        self.lib._ok(self.lib.L.spmv_plan_get_stats(self.h, ctypes.byref(st)), "spmv_plan_get_stats")
+        return st.as_dict()
+
+    def set_timing(self, on: bool) -> None:
+        self.lib._ok(self.lib.L.spmv_plan_set_timing(self.h, int(on)), "spmv_plan_set_timing")
+
+    def timing(self):
+        mean, tot, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        self.lib._ok(self.lib.L.spmv_plan_get_timing(self.h, ctypes.byref(mean), ctypes.byref(tot),
+                                                     ctypes.byref(n)), "spmv_plan_get_timing")
+        return mean.value, tot.value, n.value
+
+    def destroy(self) -> None:
+        if self.h:
+            self.lib.L.spmv_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        if torch is not None and torch.cuda.is_available():
+            return torch.cuda.current_stream().cuda_stream
+        return None
+    return getattr(stream, "cuda_stream", stream)
+
+
+def gen_banded(lib: Lib, n: int, width: int = 16, seed: int = 2, device: str = "cuda"):
+    """Config 2 matrix on the GPU: returns (row_ptr, col, val) torch tensors."""
+    rp = torch.empty(n + 1, dtype=torch.int32, device=device)
+    col = torch.empty(n * width, dtype=torch.int32, device=device)
+    val = torch.empty(n * width, dtype=_torch_dtype(lib.dtype), device=device)
+    lib._ok(lib.L.spmv_gen_banded(n, width, seed, rp.data_ptr(), col.data_ptr(), val.data_ptr(),
+                                  _stream_ptr(None)), "spmv_gen_banded")
+    return rp, col, val
+
+
+def gen_powerlaw(lib: Lib, n: int, m: int, nnz: int, seed: int = 4, max_len: int = 65536,
+                 row_begin: int = 0, row_end: int | None = None, device: str = "cuda"):
+    """Config 3 matrix (or rows [row_begin,row_end) of it) on the GPU.
+    Row lengths come from seed, columns/values from seed+1 (seeds 4, 5)."""
+    rp_full, scale = lib.powerlaw_row_ptr(n, nnz, min(max_len, m), seed)
+    row_end = n if row_end is None else row_end
+    rp_h = (rp_full[row_begin:row_end + 1].astype(np.int64) - int(rp_full[row_begin])).astype(np.uint32)
+    z = int(rp_h[-1])
+    rp = torch.from_numpy(rp_h.view(np.int32)).to(device)
+    col = torch.empty(max(z, 1), dtype=torch.int32, device=device)
+    val = torch.empty(max(z, 1), dtype=_torch_dtype(lib.dtype), device=device)
+    lib._ok(lib.L.spmv_gen_fill(row_end - row_begin, m, seed + 1, row_begin, rp.data_ptr(), col.data_ptr(),
+                                val.data_ptr(), _stream_ptr(None)), "spmv_gen_fill")
+    return rp, col[:z], val[:z], scale
+
+
+def gen_vector(lib: Lib, n: int, seed: int = 6, lo: float = 0.0, hi: float = 1.0, offset: int = 0,
+               device: str = "cuda"):
+    x = torch.empty(max(n, 1), dtype=_torch_dtype(lib.dtype), device=device)
+    lib._ok(lib.L.spmv_gen_vector(n, seed, offset, lo, hi, x.data_ptr(), _stream_ptr(None)), "spmv_gen_vector")
+    return x[:n]
+
+
+def _torch_dtype(dtype):
+    return torch.float64 if np.dtype(dtype) == np.float64 else torch.float32
+
+
+def load(dtype=np.float64) -> Lib:
+    key = np.dtype(dtype).str
+    if key not in _LIBS:
+        _LIBS[key] = Lib(dtype)
+    return _LIBS[key]

@@ -1,0 +1,125 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every function include/*.h declares,
+and its host-only logic (partitioning, generators' row structure, verification,
+storage_overhead) behaves like the reference. No compute call touches a GPU here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import spmv_hw
+from conftest import ROOT
+
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("csr_hw_wrapper.h",)]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(", text, flags=re.M):
+            if m.group(1) not in ("if", "defined"):
+                names.add(m.group(1))
+    return names
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_library_exports_every_declared_symbol(dtype):
+    path = spmv_hw.lib_path(dtype)
+    assert os.path.exists(path), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    declared = declared_functions()
+    assert len(declared) >= 20
+    missing = declared - exported
+    assert not missing, f"declared but not exported: {sorted(missing)}"
+    assert set(spmv_hw.EXPORTS) == declared
+    lib = spmv_hw.load(dtype)
+    assert lib.L.spmv_hw_value_bytes() == np.dtype(dtype).itemsize
+
+
+def test_reference_names_have_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", spmv_hw.lib_path(np.float64)], check=True,
+                         capture_output=True, text=True).stdout
+    for name in ("create_csr_hw_matrix", "spmv_hw", "create_csr_hw_x_vector", "delete_csr_hw_matrix",
+                 "storage_overhead", "verification"):
+        assert re.search(rf"\bT {name}$", out, flags=re.M), name
+
+
+def test_units_from_env(monkeypatch):
+    lib = spmv_hw.load(np.float64)
+    monkeypatch.delenv("SPMV_NGPUS", raising=False)
+    assert lib.units() == 1
+    monkeypatch.setenv("SPMV_NGPUS", "8")
+    assert lib.units() == 8
+
+
+@pytest.mark.parametrize("units", [1, 2, 3, 4, 8])
+def test_partition_is_contiguous_and_nnz_balanced(units):
+    lib = spmv_hw.load(np.float64)
+    rp, _ = lib.powerlaw_row_ptr(200_000, 3_200_000, 65536, 4)
+    b = lib.partition_rows(rp, units)
+    assert b[0] == 0 and b[-1] == 200_000 and np.all(np.diff(b.astype(np.int64)) >= 0)
+    per = np.diff(rp[b].astype(np.int64))
+    assert per.sum() == 3_200_000
+    longest = int(np.diff(rp.astype(np.int64)).max())
+    assert per.max() - 3_200_000 / units <= longest + 1
+
+
+def test_partition_degenerate_inputs():
+    lib = spmv_hw.load(np.float64)
+    rp = np.array([0, 0, 0, 5, 5], np.uint32)  # all nnz in one row
+    b = lib.partition_rows(rp, 3)
+    assert b[0] == 0 and b[-1] == 4 and np.all(np.diff(b.astype(np.int64)) >= 0)
+    rp = np.zeros(1, np.uint32)  # zero rows
+    assert list(lib.partition_rows(rp, 2)) == [0, 0, 0]
+
+
+def test_powerlaw_row_ptr_exact_and_heavy_tailed():
+    lib = spmv_hw.load(np.float64)
+    n, z = 1_000_000, 16_000_000
+    rp, s = lib.powerlaw_row_ptr(n, z, 65536, 4)
+    lens = np.diff(rp.astype(np.int64))
+    assert rp[-1] == z and lens.min() >= 1 and lens.max() <= 65536
+    assert 7.5 < s < 9.0
+    # Pareto(alpha=2) tail: P(l >= k) ~ (s/k)^2
+    k = 128
+    assert abs((lens >= k).mean() / (s / k) ** 2 - 1) < 0.15
+    rp2, s2 = lib.powerlaw_row_ptr(n, z, 65536, 4)
+    assert np.array_equal(rp, rp2) and s == s2  # deterministic
+
+
+def test_powerlaw_rejects_impossible_request():
+    lib = spmv_hw.load(np.float64)
+    with pytest.raises(RuntimeError):
+        lib.powerlaw_row_ptr(10, 5, 16, 1)  # fewer nnz than rows
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_verification_semantics(dtype, capfd):
+    """csr_hw.cpp:1571-1590: abs threshold 1e-5, NaN is an error."""
+    lib = spmv_hw.load(dtype)
+    a = np.array([1.0, 2.0, 3.0, 4.0], dtype)
+    assert lib.verification(a, a.copy()) == 0
+    b = a.copy()
+    b[1] += dtype(2e-5)
+    b[2] = np.nan
+    assert lib.verification(a, b) == 1
+    assert "Total errors : 2" in capfd.readouterr().out
+
+
+def test_storage_overhead_uses_64bit_sums():
+    """csr_hw.cpp:1401-1409 with the 32-bit overflow fixed."""
+    lib = spmv_hw.load(np.float64)
+    m = lib.csr_hw_matrix()
+    nr_ci = (spmv_hw.IndexType * 1)(40_000_000)
+    nr_val = (spmv_hw.IndexType * 1)(80_000_000)
+    m.nr_ci = ctypes.cast(nr_ci, ctypes.POINTER(spmv_hw.IndexType))
+    m.nr_val = ctypes.cast(nr_val, ctypes.POINTER(spmv_hw.IndexType))
+    m.blocks = 1
+    mb = lib.storage_overhead(ctypes.pointer(m))
+    expect = (5 * 32 + 120_000_000 * 128) / (8.0 * 1024 * 1024)
+    assert mb == pytest.approx(expect, rel=1e-12)

@@ -1,0 +1,234 @@
+"""Parity of the MI355X HIP path (through the C-ABI) with the CPU oracle.
+
+Tolerances (BASELINE.json north_star): componentwise-scaled error max_i |dy_i| / (|A||x|)_i
+<= 1e-6 for fp64 and <= 1e-4 for fp32. The HIP kernels add in a different order than spmv_gold
+(segmented wave scan, tile partials), so results are not bitwise equal to the oracle; fp64 is
+additionally held to 1e-12, which any wrong row or lost partial would exceed by many orders.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import spmv_hw
+from conftest import DTYPES, FIXTURES, GOLDEN, golden_arrays, manifest
+
+pytestmark = pytest.mark.gpu
+
+TOL = {np.dtype(np.float64): 1e-6, np.dtype(np.float32): 1e-4}
+TIGHT = {np.dtype(np.float64): 1e-12, np.dtype(np.float32): 2e-6}
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+def to_dev(torch, a):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).cuda()
+
+
+def run_device(torch, lib, row_ptr, col, val, x, nr_cols, poison=True):
+    plan = spmv_hw.Plan.from_device(lib, to_dev(torch, row_ptr), to_dev(torch, col if len(col) else np.zeros(1, np.uint32)),
+                                    to_dev(torch, val if len(val) else np.zeros(1, lib.dtype)), nr_cols)
+    n = len(row_ptr) - 1
+    y = torch.full((max(n, 1),), float("nan") if poison else 0.0, dtype=spmv_hw._torch_dtype(lib.dtype), device="cuda")
+    plan.run(to_dev(torch, x if len(x) else np.zeros(1, lib.dtype)), y)
+    torch.cuda.synchronize()
+    out = y.cpu().numpy()[:n]
+    stats = plan.stats()
+    plan.destroy()
+    return out, stats
+
+
+def check(row_ptr, col, val, x, y_ref, y, dtype):
+    assert not np.any(np.isnan(y) & ~np.isnan(y_ref)), "a row was not written"
+    err = oracle.scaled_error(row_ptr, col, val, x, y_ref, y)
+    assert err <= TOL[np.dtype(dtype)], err
+    assert err <= TIGHT[np.dtype(dtype)], err
+    return err
+
+
+def random_csr(rng, n, m, lens, dtype):
+    lens = np.asarray(lens, np.int64)
+    row_ptr = np.zeros(n + 1, np.int64)
+    row_ptr[1:] = np.cumsum(lens)
+    z = int(row_ptr[-1])
+    col = np.empty(z, np.uint32)
+    for i in range(n):
+        k = int(lens[i])
+        if k:
+            col[row_ptr[i]:row_ptr[i + 1]] = np.sort(rng.choice(m, size=min(k, m), replace=k > m))
+    val = rng.uniform(-1, 1, size=z).astype(dtype)
+    x = rng.uniform(0, 1, size=m).astype(dtype)
+    return row_ptr.astype(np.uint32), col, val, x
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("dtype,tag", DTYPES)
+def test_golden_fixtures_device_plan(torch, name, dtype, tag):
+    lib = spmv_hw.load(dtype)
+    path = os.path.join(GOLDEN, manifest()[name]["file"])
+    _, c, row_ptr, col, val, _ = oracle.read_csr(path, dtype)
+    x, y_gold = golden_arrays(name, tag)
+    y, _ = run_device(torch, lib, row_ptr, col, val, x, c)
+    check(row_ptr, col, val, x, y_gold, y, dtype)
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("dtype,tag", DTYPES)
+@pytest.mark.parametrize("units", [1, 2, 3])
+def test_reference_api_flow(torch, monkeypatch, name, dtype, tag, units):
+    """main.cpp:46-97 through the drop-in API: create_csr_hw_matrix -> create_csr_hw_x_vector ->
+    spmv_hw (accumulates into a zeroed y_fpga) -> verification -> delete_*; units = virtual
+    "Compute Units" sharing the one GPU of the box."""
+    monkeypatch.setenv("SPMV_NGPUS", str(units))
+    lib = spmv_hw.load(dtype)
+    path = os.path.join(GOLDEN, manifest()[name]["file"])
+    r, c, row_ptr, col, val, _ = oracle.read_csr(path, dtype)
+    x, y_gold = golden_arrays(name, tag)
+    m = lib.make_csr_matrix(row_ptr, col, val, c)
+    hw_matrix, bitmap = lib.create_csr_hw_matrix(m)
+    assert hw_matrix[0].contents.blocks == 1
+    assert hw_matrix[0].contents.nr_cols[0] == c
+    hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(x), hw_matrix[0].contents.blocks,
+                                    hw_matrix[0].contents.nr_cols)
+    y_fpga = np.zeros(r, dtype)
+    yv = lib.make_csr_vector(y_fpga)
+    lib.spmv_hw(hw_matrix, hx, yv, bitmap)
+    y = np.ctypeslib.as_array(yv.values, shape=(r,)).copy()
+    check(row_ptr, col, val, x, y_gold, y, dtype)
+    if dtype == np.float64:
+        assert lib.verification(y_gold, y) == 0
+    # bitmap[0][row] == row is empty (csr_hw.cpp:340-347)
+    empty = np.diff(row_ptr.astype(np.int64)) == 0
+    assert np.array_equal(np.ctypeslib.as_array(bitmap[0], shape=(r,)), empty)
+    total_mb = sum(lib.storage_overhead(hw_matrix[u]) for u in range(units))
+    assert total_mb > 0
+    # spmv_hw accumulates: a second call doubles y
+    lib.spmv_hw(hw_matrix, hx, yv, bitmap)
+    y2 = np.ctypeslib.as_array(yv.values, shape=(r,))
+    np.testing.assert_allclose(y2, 2 * y, rtol=1e-5 if dtype == np.float32 else 1e-12, atol=1e-30)
+    lib.delete_csr_hw_matrix(hw_matrix)
+    lib.free_bitmap(bitmap)
+    lib.delete_csr_hw_x_vector(hx)
+
+
+EDGE_CASES = {
+    # name: (n, m, lengths-builder)
+    "tile_aligned_rows": (64, 4096, lambda rng: np.full(64, 512)),
+    "one_entry": (1, 1, lambda rng: np.array([1])),
+    "nnz_511": (7, 300, lambda rng: np.array([100, 100, 100, 100, 100, 11, 0])),
+    "nnz_513": (3, 600, lambda rng: np.array([0, 513, 0])),
+    "long_row_100k": (5, 200_000, lambda rng: np.array([3, 100_000, 0, 7, 1])),
+    "mostly_empty": (5000, 5000, lambda rng: (rng.random(5000) < 0.02) * rng.integers(1, 40, 5000)),
+    "leading_empty": (1000, 1000, lambda rng: np.r_[np.zeros(600, int), rng.integers(1, 9, 400)]),
+    "all_empty": (100, 100, lambda rng: np.zeros(100, int)),
+    "mixed_powerlaw": (20000, 20000, lambda rng: np.minimum(np.floor(8 * rng.random(20000) ** -0.5), 5000)),
+    "rows_ending_at_lane_edges": (512, 2048, lambda rng: np.tile([4, 3, 1, 8, 16, 64, 128, 32], 64)),
+}
+
+
+@pytest.mark.parametrize("case", sorted(EDGE_CASES))
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_edge_cases(torch, case, dtype):
+    rng = np.random.default_rng(abs(hash(case)) % 2**32)
+    n, m, lens_fn = EDGE_CASES[case]
+    row_ptr, col, val, x = random_csr(rng, n, m, lens_fn(rng), dtype)
+    lib = spmv_hw.load(dtype)
+    y_ref = oracle.spmv_gold(row_ptr, col, val, x)
+    y, st = run_device(torch, lib, row_ptr, col, val, x, m)
+    check(row_ptr, col, val, x, y_ref, y, dtype)
+    assert st["nr_nzeros"] == row_ptr[-1]
+    assert st["nr_nonempty_rows"] == int((np.diff(row_ptr.astype(np.int64)) > 0).sum())
+
+
+def test_nan_in_unused_x_does_not_leak(torch):
+    """Padding entries use column 0; a non-finite x[0] must not reach any row that does not
+    reference column 0 (SURVEY B-edge: padded FPGA entries read x[0] too)."""
+    rng = np.random.default_rng(7)
+    n, m = 300, 1000
+    row_ptr, col, val, x = random_csr(rng, n, m, rng.integers(1, 9, n), np.float64)
+    col[col == 0] = 1
+    x[0] = np.nan
+    y, _ = run_device(torch, spmv_hw.load(np.float64), row_ptr, col, val, x, m)
+    assert not np.any(np.isnan(y))
+
+
+def test_out_of_range_column_is_rejected(torch):
+    lib = spmv_hw.load(np.float64)
+    row_ptr = np.array([0, 2], np.uint32)
+    col = np.array([0, 5], np.uint32)
+    with pytest.raises(RuntimeError, match="out of range"):
+        spmv_hw.Plan.from_device(lib, to_dev(torch, row_ptr), to_dev(torch, col),
+                                 to_dev(torch, np.ones(2)), 5)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_deterministic(torch, dtype):
+    rng = np.random.default_rng(3)
+    row_ptr, col, val, x = random_csr(rng, 30000, 30000, np.minimum(np.floor(8 * rng.random(30000) ** -0.5), 3000), dtype)
+    lib = spmv_hw.load(dtype)
+    y1, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
+    y2, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
+    assert np.array_equal(y1.view(np.uint8), y2.view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_synthetic_banded_vs_oracle(torch, dtype):
+    lib = spmv_hw.load(dtype)
+    n = 200_000
+    rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
+    x = spmv_hw.gen_vector(lib, n, seed=3)
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    h = [t.cpu().numpy() for t in (rp, col, val, x, y)]
+    row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
+    assert np.all(np.diff(row_ptr.astype(np.int64)) == 16)
+    check(row_ptr, c, v, xx, oracle.spmv_gold(row_ptr, c, v, xx), yy, dtype)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_synthetic_powerlaw_vs_oracle(torch, dtype):
+    """Config-3 shape scaled to 1M rows / 16M nnz (same generator, same tail)."""
+    lib = spmv_hw.load(dtype)
+    n, z = 1_000_000, 16_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    row_ptr = rp.cpu().numpy().view(np.uint32)
+    c, v, xx, yy = col.cpu().numpy().view(np.uint32), val.cpu().numpy(), x.cpu().numpy(), y.cpu().numpy()
+    assert row_ptr[-1] == z and c.max() < n
+    lens = np.diff(row_ptr.astype(np.int64))
+    assert np.all(np.diff(c.astype(np.int64))[np.ones(z - 1, bool) & ~np.isin(np.arange(1, z), row_ptr)] > 0)
+    assert lens.max() > 1000
+    check(row_ptr, c, v, xx, oracle.spmv_gold(row_ptr, c, v, xx), yy, dtype)
+
+
+def test_row_slices_match_whole_matrix(torch):
+    """Plans over nnz-balanced row slices (the multi-unit path) concatenate to the full y."""
+    lib = spmv_hw.load(np.float64)
+    rng = np.random.default_rng(11)
+    n = 50_000
+    row_ptr, col, val, x = random_csr(rng, n, n, np.minimum(np.floor(8 * rng.random(n) ** -0.5), 4000), np.float64)
+    y_ref = oracle.spmv_gold(row_ptr, col, val, x)
+    for units in (2, 4, 8):
+        b = lib.partition_rows(row_ptr, units)
+        parts = []
+        for u in range(units):
+            r0, r1 = int(b[u]), int(b[u + 1])
+            rp = row_ptr[r0:r1 + 1]
+            y, _ = run_device(torch, lib, (rp - rp[0]).astype(np.uint32), col[rp[0]:rp[-1]], val[rp[0]:rp[-1]], x, n)
+            parts.append(y)
+        check(row_ptr, col, val, x, y_ref, np.concatenate(parts), np.float64)

@@ -1,0 +1,34 @@
+#!/usr/bin/env bash
+# One gpurun session: each GPU step under its own time limit; stop at the first step that
+# faults, aborts, segfaults or times out (exit 124/134/137/139), keep going after plain test
+# failures so the bench and profile still run. Usage: tools/gpu_session.sh <tag> [steps...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}; shift || true
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+STEPS=${*:-"tests smoke bench prof"}
+export TMPDIR=/tmp
+fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a "$OUT/session.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL step $name rc=$rc; stopping" | tee -a "$OUT/session.log"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    bench32) run bench_f32 600 python bench.py --dtype f32 --no-cpu ;;
+    banded) run bench_banded 300 python bench.py --workload banded ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "session done" | tee -a "$OUT/session.log"
