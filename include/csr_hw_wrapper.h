@@ -93,6 +93,9 @@ int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *matrix
 /* d_y[0:nr_rows) = A * d_x  (overwrite; empty rows get 0). Asynchronous on `stream`. */
 int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, void *stream);
 int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
+/* Kernel variant bits (performance experiments; results are identical for every variant):
+ * bit 0 = non-temporal streamed loads (default on), bit 1 = non-temporal y stores. */
+int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */
 int spmv_plan_set_timing(spmv_plan *plan, int enable);
@@ -113,9 +116,10 @@ int spmv_gen_banded(IndexType n, IndexType width, uint64_t seed, IndexType *d_ro
  * sum(l) == nnz exactly (residual spread as +-1 over the last rows). Writes h_row_ptr[n+1]. */
 int spmv_gen_powerlaw_row_ptr(IndexType n, uint64_t nnz, IndexType max_len, uint64_t seed,
                               IndexType *h_row_ptr, double *scale_out);
-/* Fill columns/values of rows [0,n) given d_row_ptr (device): row i with l non-zeros gets
- * columns floor((j*m + r_ij) / l), r_ij = hash(seed,i,j) mod m (sorted, unique, spread over
- * [0,m)), values U(-1,1). Row i's entries depend only on (seed, i + row_offset, l, m). */
+/* Fill columns/values of rows [0,n) given d_row_ptr (device): row i with l non-zeros splits
+ * [0,m) into l integer strata [floor(j*m/l), floor((j+1)*m/l)) and draws entry j uniformly in
+ * stratum j (hash(seed,i,j)): columns strictly increase and spread over [0,m) (needs l <= m).
+ * Values U(-1,1). Row i's entries depend only on (seed, i + row_offset, l, m). */
 int spmv_gen_fill(IndexType n, IndexType m, uint64_t seed, uint64_t row_offset,
                   const IndexType *d_row_ptr, IndexType *d_col, ValueType *d_val, void *stream);
 /* d_x[i] = lo + (hi-lo)*u_i, u_i = splitmix64(seed, i + offset) in [0,1). */

@@ -43,7 +43,7 @@ __global__ void k_gen_banded(IndexType n, IndexType w, uint64_t seed, IndexType 
     }
 }
 
-// row i: l = row_ptr[i+1]-row_ptr[i]; entry j -> column floor((j*m + r)/l), r = h mod m
+// row i: l = row_ptr[i+1]-row_ptr[i]; entry j -> a uniform column of stratum j of l equal strata
 __global__ void k_gen_fill(IndexType n, IndexType m, uint64_t seed, uint64_t row_offset,
                            const IndexType *row_ptr, IndexType *col, ValueType *val)
 {
@@ -54,8 +54,9 @@ __global__ void k_gen_fill(IndexType n, IndexType m, uint64_t seed, uint64_t row
     const uint64_t gi = i + row_offset;
     for (IndexType j = 0; j < l; ++j) {
         const uint64_t h = hash3(seed, gi, j);
-        const uint64_t r = h % m;
-        col[b + j] = (IndexType)(((uint64_t)j * m + r) / l);
+        // stratum j = [floor(j*m/l), floor((j+1)*m/l)): disjoint, so columns strictly increase
+        const uint64_t lo = (uint64_t)j * m / l, hi = ((uint64_t)j + 1) * m / l;
+        col[b + j] = (IndexType)(hi > lo ? lo + h % (hi - lo) : lo % m);
         val[b + j] = (ValueType)(2.0 * u01(splitmix64(h)) - 1.0);
     }
 }

@@ -24,23 +24,48 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Streamed (read-once) loads: NT=true marks them non-temporal so they do not displace the x
+// vector from L2 / Infinity Cache (MI355X_MICROARCH.md "nt-weights").
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T *p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T *p, T v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
 // 4 consecutive logical entries [kb + 4*lane, +4) of a wave step.
+template <bool NT>
 __device__ __forceinline__ void load_vals(const double *__restrict__ val, uint64_t kb, int lane,
                                           double (&v)[4])
 {
     // fp64 pair-interleaved layout: dev[kb + j*128 + 2*lane + i] = logical[kb + 4*lane + 2*j + i]
-    const double2 a = *reinterpret_cast<const double2 *>(val + kb + 2 * lane);
-    const double2 b = *reinterpret_cast<const double2 *>(val + kb + 128 + 2 * lane);
+    const f64x2 a = ld<NT>(reinterpret_cast<const f64x2 *>(val + kb + 2 * lane));
+    const f64x2 b = ld<NT>(reinterpret_cast<const f64x2 *>(val + kb + 128 + 2 * lane));
     v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
 }
+template <bool NT>
 __device__ __forceinline__ void load_vals(const float *__restrict__ val, uint64_t kb, int lane,
                                           float (&v)[4])
 {
-    const float4 a = *reinterpret_cast<const float4 *>(val + kb + 4 * lane);
+    const f32x4 a = ld<NT>(reinterpret_cast<const f32x4 *>(val + kb + 4 * lane));
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
 
-template <typename V>
+template <bool NTY, typename V>
 __device__ __forceinline__ void emit(V sum, uint32_t r, bool to_head, V *__restrict__ head,
                                      uint64_t t, const uint32_t *__restrict__ row_id,
                                      V *__restrict__ y)
@@ -48,10 +73,11 @@ __device__ __forceinline__ void emit(V sum, uint32_t r, bool to_head, V *__restr
     if (to_head)
         head[t] = sum;
     else
-        y[row_id ? row_id[r] : r] = sum;
+        st<NTY>(y + (row_id ? row_id[r] : r), sum);
 }
 
-template <typename V, int U>
+// VAR bit 0: non-temporal streamed loads (col, val, row-end bits); bit 1: non-temporal y stores
+template <typename V, int U, int VAR>
 __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     const uint32_t *__restrict__ col, const V *__restrict__ val, const uint32_t *__restrict__ rowend,
     const uint32_t *__restrict__ tile_info, const uint32_t *__restrict__ row_id,
@@ -71,10 +97,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t kb = k0 + (uint64_t)u * kStep;
-        const uint4 cc = *reinterpret_cast<const uint4 *>(col + kb + 4 * lane);
+        const u32x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u32x4 *>(col + kb + 4 * lane));
         c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
-        load_vals(val, kb, lane, v[u]);
-        fl[u] = (rowend[(kb >> 5) + (lane >> 3)] >> ((lane & 7) * 4)) & 0xFu;
+        load_vals<(VAR & 1) != 0>(val, kb, lane, v[u]);
+        fl[u] = (ld<(VAR & 1) != 0>(rowend + (kb >> 5) + (lane >> 3)) >> ((lane & 7) * 4)) & 0xFu;
     }
     V xv[U][4];
 #pragma unroll
@@ -137,7 +163,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
         for (int j = 0; j < 4; ++j) {
             run = run + p[j];
             if (f & (1u << j)) {
-                emit(run, r, to_head, head, t, row_id, y);
+                emit<(VAR & 2) != 0>(run, r, to_head, head, t, row_id, y);
                 to_head = false;
                 ++r;
                 run = V(0);
@@ -203,10 +229,8 @@ __global__ void k_pack(const IndexType *__restrict__ col_src, const V *__restric
         return;
     const bool in = k < nnz;
     uint32_t c = in ? col_src[k] : 0u;
-    if (c >= ncols) {  // never let an out-of-range index reach the gather
-        atomicOr(bad, 1u);
+    if (c >= ncols)  // validated before packing; never let an out-of-range index reach a gather
         c = 0u;
-    }
     col[k] = c;
     uint64_t dst = k;
     if (sizeof(V) == 8) {
@@ -224,9 +248,17 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
         return hipSuccess;
     const uint64_t waves_per_block = kBlockThreads / kWave;
     const uint64_t blocks = (p.ntiles + waves_per_block - 1) / waves_per_block;
-    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps>), dim3((unsigned)blocks),
-                       dim3(kBlockThreads), 0, s, p.d_col, p.d_val, p.d_rowend, p.d_tile_info,
-                       p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.d_tflags, p.nnz, p.ntiles);
+#define SPMV_LAUNCH(VAR)                                                                          \
+    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps, VAR>), dim3((unsigned)blocks),         \
+                       dim3(kBlockThreads), 0, s, p.d_col, p.d_val, p.d_rowend, p.d_tile_info,      \
+                       p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.d_tflags, p.nnz, p.ntiles)
+    switch (p.variant & 3) {
+    case 0: SPMV_LAUNCH(0); break;
+    case 1: SPMV_LAUNCH(1); break;
+    case 2: SPMV_LAUNCH(2); break;
+    default: SPMV_LAUNCH(3); break;
+    }
+#undef SPMV_LAUNCH
     return hipGetLastError();
 }
 
@@ -237,6 +269,22 @@ hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s)
     const uint64_t blocks = (p.ntiles + 255) / 256;
     hipLaunchKernelGGL((k_fixup<ValueType>), dim3((unsigned)blocks), dim3(256), 0, s, p.d_tflags,
                        p.d_head, p.d_tail, p.d_tile_info, p.d_row_id, d_y, p.ntiles);
+    return hipGetLastError();
+}
+
+__global__ void k_validate(const IndexType *__restrict__ col, uint64_t nnz, uint32_t ncols,
+                           uint32_t *__restrict__ bad)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nnz && col[k] >= ncols)
+        atomicOr(bad, 1u);
+}
+
+hipError_t launch_validate(const IndexType *d_col, uint64_t nnz, uint32_t ncols, uint32_t *d_bad, hipStream_t s)
+{
+    if (nnz == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_validate, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_col, nnz, ncols, d_bad);
     return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@
 //   create_block_matrix +
 //   generate_balanced_hw_submatrix (:190-318) -> k_pack on the GPU (O(nnz), coalesced)
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
@@ -20,59 +21,44 @@ static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 const char *get_error() { return g_err.c_str(); }
 
-int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,
-                                 const IndexType *h_row_ptr, const IndexType *col_src,
-                                 const ValueType *val_src, bool src_on_device, hipStream_t s)
+// Which kernel a plan uses: env SPMV_HW_KERNEL = tiles | sweep | auto (default).
+static int requested_kernel()
 {
-    *out = nullptr;
-    if (nr_rows > 0 && h_row_ptr[0] != 0) {
-        set_error("row_ptr must be rebased to 0");
-        return 1;
-    }
-    const uint64_t nnz = nr_rows ? h_row_ptr[nr_rows] : 0;
-    for (IndexType r = 0; r < nr_rows; ++r) {
-        if (h_row_ptr[r + 1] < h_row_ptr[r]) {
-            set_error("row_ptr is not non-decreasing at row " + std::to_string(r));
-            return 1;
-        }
-    }
-    if (nnz > 0 && nr_cols == 0) {
-        set_error("matrix has non-zeros but zero columns");
-        return 1;
-    }
-    SPMV_TRY(hipSetDevice(device));
+    const char *e = std::getenv("SPMV_HW_KERNEL");
+    if (!e || !*e || !std::strcmp(e, "auto"))
+        return -1;
+    if (!std::strcmp(e, "tiles"))
+        return kKernelTiles;
+    if (!std::strcmp(e, "sweep"))
+        return kKernelSweep;
+    return -1;
+}
 
-    std::unique_ptr<spmv_plan> p(new spmv_plan());
-    p->device = device;
-    p->nr_rows = nr_rows;
-    p->nr_cols = nr_cols;
-    p->nnz = nnz;
-    p->nnz_pad = (nnz + kTileNnz - 1) / kTileNnz * kTileNnz;
-    p->ntiles = p->nnz_pad / kTileNnz;
+// Flagged-tile representation (kernel 0): row-end bitmap, tile table, packed col/val.
+static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType *d_col_src,
+                       const ValueType *d_val_src, hipStream_t s)
+{
+    const IndexType nr_rows = p.nr_rows;
+    const uint64_t nnz = p.nnz;
+    p.nnz_pad = (nnz + kTileNnz - 1) / kTileNnz * kTileNnz;
+    p.ntiles = p.nnz_pad / kTileNnz;
 
-    // ---- host metadata: row-end bitmap, non-empty row map, tile table ----
-    std::vector<uint32_t> rowend(p->nnz_pad / 32, 0u);
+    std::vector<uint32_t> rowend(p.nnz_pad / 32, 0u);
     std::vector<uint32_t> row_id;
-    uint64_t nzr = 0;
-    for (IndexType r = 0; r < nr_rows; ++r)
-        if (h_row_ptr[r + 1] > h_row_ptr[r])
-            ++nzr;
-    p->nzr = nzr;
-    p->has_empty = nzr < nr_rows;
-    if (p->has_empty)
-        row_id.reserve(nzr);
+    if (p.has_empty)
+        row_id.reserve(p.nzr);
     for (IndexType r = 0; r < nr_rows; ++r) {
         if (h_row_ptr[r + 1] > h_row_ptr[r]) {
             const uint64_t e = h_row_ptr[r + 1] - 1ull;
             rowend[e >> 5] |= 1u << (e & 31);
-            if (p->has_empty)
+            if (p.has_empty)
                 row_id.push_back(r);
         }
     }
-    std::vector<uint32_t> tile_info(p->ntiles + 1, 0u);
+    std::vector<uint32_t> tile_info(p.ntiles + 1, 0u);
     {
         uint64_t rr = 0, c = 0;
-        for (uint64_t t = 0; t <= p->ntiles; ++t) {
+        for (uint64_t t = 0; t <= p.ntiles; ++t) {
             const uint64_t k = t * kTileNnz;
             while (rr < nr_rows && h_row_ptr[rr + 1] <= k) {
                 if (h_row_ptr[rr + 1] > h_row_ptr[rr])
@@ -87,56 +73,113 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             tile_info[t] = (uint32_t)(c << 1) | (cont ? 1u : 0u);
         }
     }
-
-    // ---- device buffers ----
     auto alloc = [&](void **ptr, size_t bytes) -> hipError_t {
         *ptr = nullptr;
         return bytes ? hipMalloc(ptr, bytes) : hipSuccess;
     };
-    SPMV_TRY(alloc((void **)&p->d_col, p->nnz_pad * sizeof(uint32_t)));
-    SPMV_TRY(alloc((void **)&p->d_val, p->nnz_pad * sizeof(ValueType)));
-    SPMV_TRY(alloc((void **)&p->d_rowend, rowend.size() * sizeof(uint32_t)));
-    SPMV_TRY(alloc((void **)&p->d_tile_info, tile_info.size() * sizeof(uint32_t)));
-    SPMV_TRY(alloc((void **)&p->d_head, p->ntiles * sizeof(ValueType)));
-    SPMV_TRY(alloc((void **)&p->d_tail, p->ntiles * sizeof(ValueType)));
-    SPMV_TRY(alloc((void **)&p->d_tflags, p->ntiles));
-    if (p->has_empty)
-        SPMV_TRY(alloc((void **)&p->d_row_id, row_id.size() * sizeof(uint32_t)));
-
+    SPMV_TRY(alloc((void **)&p.d_col, p.nnz_pad * sizeof(uint32_t)));
+    SPMV_TRY(alloc((void **)&p.d_val, p.nnz_pad * sizeof(ValueType)));
+    SPMV_TRY(alloc((void **)&p.d_rowend, rowend.size() * sizeof(uint32_t)));
+    SPMV_TRY(alloc((void **)&p.d_tile_info, tile_info.size() * sizeof(uint32_t)));
+    SPMV_TRY(alloc((void **)&p.d_head, p.ntiles * sizeof(ValueType)));
+    SPMV_TRY(alloc((void **)&p.d_tail, p.ntiles * sizeof(ValueType)));
+    SPMV_TRY(alloc((void **)&p.d_tflags, p.ntiles));
+    if (p.has_empty)
+        SPMV_TRY(alloc((void **)&p.d_row_id, row_id.size() * sizeof(uint32_t)));
     if (!rowend.empty())
-        SPMV_TRY(hipMemcpyAsync(p->d_rowend, rowend.data(), rowend.size() * 4, hipMemcpyHostToDevice, s));
-    SPMV_TRY(hipMemcpyAsync(p->d_tile_info, tile_info.data(), tile_info.size() * 4, hipMemcpyHostToDevice, s));
-    if (p->has_empty && !row_id.empty())
-        SPMV_TRY(hipMemcpyAsync(p->d_row_id, row_id.data(), row_id.size() * 4, hipMemcpyHostToDevice, s));
+        SPMV_TRY(hipMemcpyAsync(p.d_rowend, rowend.data(), rowend.size() * 4, hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipMemcpyAsync(p.d_tile_info, tile_info.data(), tile_info.size() * 4, hipMemcpyHostToDevice, s));
+    if (p.has_empty && !row_id.empty())
+        SPMV_TRY(hipMemcpyAsync(p.d_row_id, row_id.data(), row_id.size() * 4, hipMemcpyHostToDevice, s));
+    if (p.nnz_pad)
+        SPMV_TRY(launch_pack(d_col_src, d_val_src, nnz, p.nnz_pad, p.nr_cols, p.d_col, p.d_val, nullptr, s));
+    // pageable host vectors above go out of scope: make the copies complete first
+    SPMV_TRY(hipStreamSynchronize(s));
+    return 0;
+}
 
-    if (p->nnz_pad) {
-        uint32_t *d_bad = nullptr;
-        SPMV_TRY(hipMalloc((void **)&d_bad, sizeof(uint32_t)));
-        SPMV_TRY(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s));
-        if (src_on_device) {
-            SPMV_TRY(launch_pack(col_src, val_src, nnz, p->nnz_pad, nr_cols, p->d_col, p->d_val, d_bad, s));
-        } else {
-            IndexType *d_cs = nullptr;
-            ValueType *d_vs = nullptr;
-            SPMV_TRY(alloc((void **)&d_cs, nnz * sizeof(IndexType)));
-            SPMV_TRY(alloc((void **)&d_vs, nnz * sizeof(ValueType)));
-            if (nnz) {
-                SPMV_TRY(hipMemcpyAsync(d_cs, col_src, nnz * sizeof(IndexType), hipMemcpyHostToDevice, s));
-                SPMV_TRY(hipMemcpyAsync(d_vs, val_src, nnz * sizeof(ValueType), hipMemcpyHostToDevice, s));
-            }
-            SPMV_TRY(launch_pack(d_cs, d_vs, nnz, p->nnz_pad, nr_cols, p->d_col, p->d_val, d_bad, s));
-            SPMV_TRY(hipStreamSynchronize(s));
-            SPMV_TRY(hipFree(d_cs));
-            SPMV_TRY(hipFree(d_vs));
+int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,
+                                 const IndexType *h_row_ptr, const IndexType *col_src,
+                                 const ValueType *val_src, bool src_on_device, hipStream_t s)
+{
+    *out = nullptr;
+    if (nr_rows > 0 && h_row_ptr[0] != 0) {
+        set_error("row_ptr must be rebased to 0");
+        return 1;
+    }
+    const uint64_t nnz = nr_rows ? h_row_ptr[nr_rows] : 0;
+    uint64_t nzr = 0;
+    for (IndexType r = 0; r < nr_rows; ++r) {
+        if (h_row_ptr[r + 1] < h_row_ptr[r]) {
+            set_error("row_ptr is not non-decreasing at row " + std::to_string(r));
+            return 1;
         }
+        nzr += h_row_ptr[r + 1] > h_row_ptr[r];
+    }
+    if (nnz > 0 && nr_cols == 0) {
+        set_error("matrix has non-zeros but zero columns");
+        return 1;
+    }
+    SPMV_TRY(hipSetDevice(device));
+
+    std::unique_ptr<spmv_plan> p(new spmv_plan());
+    p->device = device;
+    p->nr_rows = nr_rows;
+    p->nr_cols = nr_cols;
+    p->nnz = nnz;
+    p->nzr = nzr;
+    p->has_empty = nzr < nr_rows;
+
+    // device copies of the CSR entries (host path: upload), validated before any kernel gathers
+    struct Tmp {
+        void *p = nullptr;
+        ~Tmp() { if (p) (void)hipFree(p); }
+    } tcol, tval, trp, tbad;
+    const IndexType *d_col = col_src;
+    const ValueType *d_val = val_src;
+    if (!src_on_device && nnz) {
+        SPMV_TRY(hipMalloc(&tcol.p, nnz * sizeof(IndexType)));
+        SPMV_TRY(hipMalloc(&tval.p, nnz * sizeof(ValueType)));
+        SPMV_TRY(hipMemcpyAsync(tcol.p, col_src, nnz * sizeof(IndexType), hipMemcpyHostToDevice, s));
+        SPMV_TRY(hipMemcpyAsync(tval.p, val_src, nnz * sizeof(ValueType), hipMemcpyHostToDevice, s));
+        d_col = (const IndexType *)tcol.p;
+        d_val = (const ValueType *)tval.p;
+    }
+    if (nnz) {
+        SPMV_TRY(hipMalloc(&tbad.p, sizeof(uint32_t)));
+        SPMV_TRY(hipMemsetAsync(tbad.p, 0, sizeof(uint32_t), s));
+        SPMV_TRY(launch_validate(d_col, nnz, nr_cols, (uint32_t *)tbad.p, s));
         uint32_t bad = 0;
-        SPMV_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, s));
+        SPMV_TRY(hipMemcpyAsync(&bad, tbad.p, sizeof(bad), hipMemcpyDeviceToHost, s));
         SPMV_TRY(hipStreamSynchronize(s));
-        SPMV_TRY(hipFree(d_bad));
         if (bad) {
             set_error("column index out of range (>= nr_cols)");
             return 1;
         }
+    }
+
+    int kernel = requested_kernel();
+    if (kernel < 0) {
+        // automatic choice: the sweep pays when x is far larger than the L2s and the columns of a
+        // row are scattered (the first two columns of sampled rows lie >= 64 apart)
+        kernel = kKernelTiles;
+        if (nnz && uint64_t(nr_cols) * sizeof(ValueType) > (32ull << 20) && nnz >= 16ull * kSweepThreads) {
+            SPMV_TRY(hipMalloc(&trp.p, (size_t(nr_rows) + 1) * sizeof(IndexType)));
+            SPMV_TRY(hipMemcpyAsync(trp.p, h_row_ptr, (size_t(nr_rows) + 1) * sizeof(IndexType),
+                                    hipMemcpyHostToDevice, s));
+            if (probe_locality((const IndexType *)trp.p, d_col, nr_rows, s, &p->locality))
+                return 1;
+            if (p->locality < 0.5)
+                kernel = kKernelSweep;
+        }
+    }
+    p->kernel = kernel;
+    if (kernel == kKernelSweep) {
+        if (build_sweep(*p, h_row_ptr, d_col, d_val, s))
+            return 1;
+    } else {
+        if (build_tiles(*p, h_row_ptr, d_col, d_val, s))
+            return 1;
     }
     SPMV_TRY(hipStreamSynchronize(s));
     *out = p.release();
@@ -152,7 +195,8 @@ spmv_plan::~spmv_plan()
     (void)hipSetDevice(device);
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
-                      (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_tflags})
+                      (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_tflags, (void *)d_s_col,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_panel_ent})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -161,6 +205,8 @@ spmv_plan::~spmv_plan()
 
 uint64_t spmv_plan::device_bytes() const
 {
+    if (kernel == kKernelSweep)
+        return ent_pad * (sizeof(uint32_t) + sizeof(uint16_t) + sizeof(ValueType)) + (npanels + 1) * 8;
     return nnz_pad * (sizeof(uint32_t) + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
            (has_empty ? nzr * 4 : 0) + ntiles * (2 * sizeof(ValueType) + 1);
 }
@@ -232,7 +278,7 @@ int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, voi
     SPMV_TRY(hipSetDevice(p->device));
     if (p->nr_rows == 0)
         return 0;
-    if (p->has_empty || p->nnz == 0)
+    if (p->kernel != kKernelSweep && (p->has_empty || p->nnz == 0))
         SPMV_TRY(hipMemsetAsync(d_y, 0, size_t(p->nr_rows) * sizeof(ValueType), s));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (p->timing) {
@@ -247,6 +293,12 @@ int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, voi
         e1 = p->ev[p->ev_used + 1];
         p->ev_used += 2;
         SPMV_TRY(hipEventRecord(e0, s));
+    }
+    if (p->kernel == kKernelSweep) {
+        SPMV_TRY(launch_sweep(*p, d_x, d_y, s));
+        if (p->timing)
+            SPMV_TRY(hipEventRecord(e1, s));
+        return 0;
     }
     SPMV_TRY(launch_spmv(*p, d_x, d_y, s));
     if (p->timing)
@@ -266,14 +318,24 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->nr_cols = p->nr_cols;
     st->nr_nzeros = p->nnz;
     st->nr_nonempty_rows = p->nzr;
-    st->nr_tiles = p->ntiles;
-    st->tile_nnz = kTileNnz;
+    st->nr_tiles = p->kernel == kKernelSweep ? p->npanels : p->ntiles;
+    st->tile_nnz = p->kernel == kKernelSweep ? (p->npanels ? p->ent_pad / p->npanels : 0) : kTileNnz;
     st->device_bytes = p->device_bytes();
     st->algorithmic_bytes = p->algorithmic_bytes();
     st->device = p->device;
     st->kernel = p->kernel;
     st->blocks = 1;
     st->lds_tiles_pct = 0;
+    return 0;
+}
+
+int spmv_plan_set_variant(spmv_plan *p, int variant)
+{
+    if (!p || variant < 0 || variant > 3) {
+        set_error("spmv_plan_set_variant: bad arguments");
+        return 1;
+    }
+    p->variant = variant;
     return 0;
 }
 

@@ -32,6 +32,12 @@ constexpr int kStep = kWave * kLaneEntries;        // 256 entries per wave step
 constexpr int kTileSteps = 2;                      // wave steps per tile
 constexpr int kTileNnz = kStep * kTileSteps;       // 512 entries per wave tile
 constexpr int kBlockThreads = 256;                 // 4 waves = 4 tiles per workgroup
+constexpr int kSweepThreads = 1024;                // panel-sweep workgroup (16 waves, one per CU)
+constexpr uint64_t kSweepLdsBytes = 160 * 1024;    // LDS of one CU holds the panel's y
+
+// plan kernels (spmv_plan_stats.kernel)
+constexpr int kKernelTiles = 0;  // flagged-tile wave kernel, x gathered through the caches
+constexpr int kKernelSweep = 2;  // panel sweep: y in LDS, columns swept in order (x from L2)
 
 // tile flags written by the main kernel, read by the fix-up kernel
 constexpr uint8_t kHasTail = 1;   // tile ends inside a row that continues in the next tile
@@ -46,6 +52,7 @@ struct spmv_plan {
     uint64_t ntiles = 0;
     bool has_empty = false;
     int kernel = 0;
+    int variant = 1;           // kernel variant bits (spmv_plan_set_variant)
 
     uint32_t *d_col = nullptr;
     ValueType *d_val = nullptr;
@@ -55,6 +62,16 @@ struct spmv_plan {
     ValueType *d_head = nullptr;
     ValueType *d_tail = nullptr;
     uint8_t *d_tflags = nullptr;
+
+    // panel-sweep representation (kernel 2, sweep.hip)
+    uint64_t npanels = 0, ent_pad = 0;
+    uint32_t panel_rmax = 0;
+    uint32_t *d_s_col = nullptr;
+    uint16_t *d_s_row = nullptr;
+    ValueType *d_s_val = nullptr;
+    uint32_t *d_panel_row = nullptr;
+    uint32_t *d_panel_ent = nullptr;
+    double locality = -1.0;    // probe result used by the automatic kernel choice
 
     // timing (HIP events around the main kernel, on the launch stream)
     bool timing = false;
@@ -77,6 +94,13 @@ hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s);
 hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, uint64_t nnz,
                        uint64_t nnz_pad, uint32_t ncols, uint32_t *d_col, ValueType *d_val,
                        uint32_t *d_bad, hipStream_t s);
+hipError_t launch_validate(const IndexType *d_col, uint64_t nnz, uint32_t ncols, uint32_t *d_bad, hipStream_t s);
+
+// sweep.hip
+hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);
+int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
+                hipStream_t s);
+int probe_locality(const IndexType *d_rp, const IndexType *d_col, IndexType n, hipStream_t s, double *frac);
 
 // plan.cpp helpers shared with the wrapper
 int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,

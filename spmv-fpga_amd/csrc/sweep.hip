@@ -1,0 +1,337 @@
+// Kernel 2 — "panel sweep": the reference's 2-D blocking turned around for MI355X.
+//
+// The reference keeps a whole column block of x in every CU's BRAM and streams that block's
+// rows through the CU, scattering each CU's compact y back on the host (spmv.cpp:169-205,
+// csr_hw.cpp:1531-1565). For a matrix whose columns are spread at random over an x far larger
+// than the 4 MiB L2 of an XCD, gathering x straight from HBM/Infinity Cache costs one L2 miss
+// per non-zero, and MI355X serves only ~55 G such misses/s (tools/hbm_calib, profiles/).
+// Here each workgroup instead owns a row panel whose y stays resident in LDS (<= 160 KiB) and
+// walks the panel's non-zeros in ascending column order. All panels sweep the columns at the
+// same pace, so the x lines in use at any moment form a narrow window that the XCD's L2 serves
+// (~265 G gathers/s, 5x the miss rate). Products are accumulated with LDS fp64 atomics; y is
+// written once per panel with coalesced stores.
+//
+// Representation (built on the GPU in O(nnz log) with a hipcub radix sort):
+//   s_col u32[ent_pad]  column of each entry, panels contiguous, ascending column per panel
+//   s_row u16[ent_pad]  row inside the panel (padding entries use the scratch slot R_p)
+//   s_val V[ent_pad]    value
+//   panel_row u32[P+1]  row range of panel p; panel_ent u32[P+1] entry range (multiples of 4)
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+
+#include "spmv_internal.hpp"
+
+namespace spmvhw {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void load4(const double *__restrict__ v, uint64_t e, double (&o)[4])
+{
+    const f64x2 a = *reinterpret_cast<const f64x2 *>(v + e);
+    const f64x2 b = *reinterpret_cast<const f64x2 *>(v + e + 2);
+    o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+}
+__device__ __forceinline__ void load4(const float *__restrict__ v, uint64_t e, float (&o)[4])
+{
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(v + e);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+}
+
+template <typename V>
+__global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
+    const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
+    const V *__restrict__ x, V *__restrict__ y)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    V *ylds = reinterpret_cast<V *>(smem);
+    const uint32_t p = blockIdx.x;
+    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
+    const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
+    for (uint32_t i = threadIdx.x; i <= R; i += kSweepThreads)
+        ylds[i] = V(0);
+    __syncthreads();
+    constexpr uint64_t kStride = 4ull * kSweepThreads;
+    uint64_t e = e0 + 4ull * threadIdx.x;
+    // two quads per thread per iteration: 8 gathers in flight
+    for (; e + kStride < e1; e += 2 * kStride) {
+        const u32x4 ca = *reinterpret_cast<const u32x4 *>(col + e);
+        const u32x4 cb = *reinterpret_cast<const u32x4 *>(col + e + kStride);
+        const u16x4 ra = *reinterpret_cast<const u16x4 *>(row + e);
+        const u16x4 rb = *reinterpret_cast<const u16x4 *>(row + e + kStride);
+        V va[4], vb[4];
+        load4(val, e, va);
+        load4(val, e + kStride, vb);
+        const V xa0 = x[ca.x], xa1 = x[ca.y], xa2 = x[ca.z], xa3 = x[ca.w];
+        const V xb0 = x[cb.x], xb1 = x[cb.y], xb2 = x[cb.z], xb3 = x[cb.w];
+        atomicAdd(&ylds[ra.x], va[0] * xa0);
+        atomicAdd(&ylds[ra.y], va[1] * xa1);
+        atomicAdd(&ylds[ra.z], va[2] * xa2);
+        atomicAdd(&ylds[ra.w], va[3] * xa3);
+        atomicAdd(&ylds[rb.x], vb[0] * xb0);
+        atomicAdd(&ylds[rb.y], vb[1] * xb1);
+        atomicAdd(&ylds[rb.z], vb[2] * xb2);
+        atomicAdd(&ylds[rb.w], vb[3] * xb3);
+    }
+    if (e < e1) {
+        const u32x4 ca = *reinterpret_cast<const u32x4 *>(col + e);
+        const u16x4 ra = *reinterpret_cast<const u16x4 *>(row + e);
+        V va[4];
+        load4(val, e, va);
+        atomicAdd(&ylds[ra.x], va[0] * x[ca.x]);
+        atomicAdd(&ylds[ra.y], va[1] * x[ca.y]);
+        atomicAdd(&ylds[ra.z], va[2] * x[ca.z]);
+        atomicAdd(&ylds[ra.w], va[3] * x[ca.w]);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < R; i += kSweepThreads)
+        y[r0 + i] = ylds[i];
+}
+
+// sort key of every entry: (panel, column bucket); one thread per row
+__global__ void k_sweep_keys(const IndexType *__restrict__ rp, const IndexType *__restrict__ col,
+                             const uint32_t *__restrict__ panel_row, uint32_t npanels, IndexType nrows,
+                             uint64_t nbuckets, uint32_t shift, uint32_t *__restrict__ keys,
+                             uint32_t *__restrict__ idx)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows)
+        return;
+    // panel of row r: last p with panel_row[p] <= r
+    uint32_t lo = 0, hi = npanels;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (panel_row[mid] <= r)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    const uint64_t pbase = (uint64_t)lo * nbuckets;
+    for (IndexType j = rp[r]; j < rp[r + 1]; ++j) {
+        keys[j] = (uint32_t)(pbase + (col[j] >> shift));
+        idx[j] = j;
+    }
+}
+
+// sorted position k -> padded position; carries column, in-panel row, value
+template <typename V>
+__global__ void k_sweep_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
+                                uint64_t nnz, uint64_t nbuckets, const IndexType *__restrict__ rp,
+                                IndexType nrows, const IndexType *__restrict__ col_src,
+                                const V *__restrict__ val_src, const uint32_t *__restrict__ panel_row,
+                                const uint32_t *__restrict__ off, const uint32_t *__restrict__ poff,
+                                uint32_t *__restrict__ s_col, uint16_t *__restrict__ s_row,
+                                V *__restrict__ s_val)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz)
+        return;
+    const uint32_t p = (uint32_t)(keys[k] / nbuckets);
+    const uint32_t j = idx[k];
+    // row of entry j: last r with rp[r] <= j (rows with entries only)
+    uint32_t lo = 0, hi = nrows;
+    while (hi - lo > 1) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (rp[mid] <= j)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    const uint64_t dst = (uint64_t)poff[p] + (k - off[p]);
+    s_col[dst] = col_src[j];
+    s_row[dst] = (uint16_t)(lo - panel_row[p]);
+    s_val[dst] = val_src[j];
+}
+
+template <typename V>
+__global__ void k_sweep_pad(uint32_t npanels, const uint32_t *__restrict__ panel_row,
+                            const uint32_t *__restrict__ off, const uint32_t *__restrict__ poff,
+                            uint32_t *__restrict__ s_col, uint16_t *__restrict__ s_row, V *__restrict__ s_val)
+{
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npanels)
+        return;
+    const uint32_t R = panel_row[p + 1] - panel_row[p];
+    for (uint64_t d = (uint64_t)poff[p] + (off[p + 1] - off[p]); d < poff[p + 1]; ++d) {
+        s_col[d] = 0;
+        s_row[d] = (uint16_t)R;  // scratch slot, never written back
+        s_val[d] = V(0);
+    }
+}
+
+// locality probe: fraction of sampled rows whose first two columns are < 64 apart
+__global__ void k_locality(const IndexType *__restrict__ rp, const IndexType *__restrict__ col, IndexType nrows,
+                           uint32_t stride, unsigned long long *__restrict__ counts)
+{
+    const uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * stride;
+    if (r >= nrows)
+        return;
+    const IndexType b = rp[r], e = rp[r + 1];
+    if (e - b < 2)
+        return;
+    const IndexType c0 = col[b], c1 = col[b + 1];
+    const IndexType d = c1 > c0 ? c1 - c0 : c0 - c1;
+    atomicAdd(&counts[0], 1ull);
+    if (d < 64)
+        atomicAdd(&counts[1], 1ull);
+}
+
+hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+{
+    if (p.npanels == 0)
+        return hipSuccess;
+    const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(ValueType);
+    hipLaunchKernelGGL((k_spmv_sweep<ValueType>), dim3((unsigned)p.npanels), dim3(kSweepThreads), lds, s,
+                       p.d_s_col, p.d_s_row, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+    return hipGetLastError();
+}
+
+// Host: panel boundaries (nnz-balanced, <= rmax rows each, a multiple of the CU count when
+// possible), then the device sort + scatter.
+int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
+                hipStream_t s)
+{
+    const IndexType n = p.nr_rows;
+    const uint64_t nnz = p.nnz;
+    const uint32_t rmax = (uint32_t)std::min<uint64_t>(kSweepLdsBytes / sizeof(ValueType) - 1, 65534);
+    int cus = 256;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, p.device) == hipSuccess && prop.multiProcessorCount > 0)
+            cus = prop.multiProcessorCount;
+    }
+    std::vector<uint32_t> prow;
+    for (uint64_t P = std::max<uint64_t>(1, (n + rmax - 1) / rmax);; ++P) {
+        if (P > 1 && P % cus)
+            P = (P + cus - 1) / cus * cus;  // whole rounds of workgroups
+        P = std::min<uint64_t>(P, std::max<uint64_t>(n, 1));
+        prow.assign(1, 0);
+        bool ok = true;
+        IndexType r = 0;
+        for (uint64_t q = 1; q <= P && ok; ++q) {
+            const uint64_t target = nnz * q / P;
+            IndexType e = (q == P) ? n : (IndexType)(std::lower_bound(h_rp, h_rp + n + 1, (IndexType)target) - h_rp);
+            e = std::max(e, r);
+            if (e - r > rmax)
+                ok = false;
+            prow.push_back(e);
+            r = e;
+        }
+        if (ok)
+            break;
+        if (P >= n) {
+            set_error("build_sweep: cannot form panels");
+            return 1;
+        }
+    }
+    const uint32_t P = (uint32_t)(prow.size() - 1);
+    std::vector<uint32_t> off(P + 1), poff(P + 1);
+    off[0] = poff[0] = 0;
+    uint32_t rmax_used = 0;
+    for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t cnt = uint64_t(h_rp[prow[q + 1]]) - h_rp[prow[q]];
+        off[q + 1] = (uint32_t)(off[q] + cnt);
+        poff[q + 1] = (uint32_t)(poff[q] + (cnt + 3) / 4 * 4);
+        rmax_used = std::max(rmax_used, prow[q + 1] - prow[q]);
+    }
+    p.npanels = P;
+    p.panel_rmax = rmax_used;
+    p.ent_pad = poff[P];
+
+    // bucket shift so that P * buckets fits 32-bit keys
+    uint32_t shift = 0;
+    while ((uint64_t(P) * ((uint64_t(p.nr_cols) >> shift) + 1)) >= (1ull << 32))
+        ++shift;
+    const uint64_t nbuckets = (uint64_t(p.nr_cols) >> shift) + 1;
+    int end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) < uint64_t(P) * nbuckets)
+        ++end_bit;
+
+    SPMV_TRY(hipMalloc((void **)&p.d_panel_row, (P + 1) * 4));
+    SPMV_TRY(hipMalloc((void **)&p.d_panel_ent, (P + 1) * 4));
+    SPMV_TRY(hipMemcpyAsync(p.d_panel_row, prow.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipMemcpyAsync(p.d_panel_ent, poff.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipMalloc((void **)&p.d_s_col, std::max<uint64_t>(p.ent_pad, 4) * 4));
+    SPMV_TRY(hipMalloc((void **)&p.d_s_row, std::max<uint64_t>(p.ent_pad, 4) * 2));
+    SPMV_TRY(hipMalloc((void **)&p.d_s_val, std::max<uint64_t>(p.ent_pad, 4) * sizeof(ValueType)));
+
+    uint32_t *d_off = nullptr, *d_poff = nullptr;
+    IndexType *d_rp = nullptr;
+    uint32_t *k0 = nullptr, *k1 = nullptr, *i0 = nullptr, *i1 = nullptr;
+    void *tmp = nullptr;
+    size_t tmp_bytes = 0;
+    auto cleanup = [&]() {
+        for (void *q : {(void *)d_off, (void *)d_poff, (void *)d_rp, (void *)k0, (void *)k1, (void *)i0,
+                        (void *)i1, tmp})
+            if (q)
+                (void)hipFree(q);
+    };
+    auto fail = [&](hipError_t e, const char *what) {
+        set_error(std::string("build_sweep: ") + what + ": " + hipGetErrorString(e));
+        cleanup();
+        return 1;
+    };
+#define SW_TRY(x)                              \
+    do {                                       \
+        hipError_t e_ = (x);                   \
+        if (e_ != hipSuccess)                  \
+            return fail(e_, #x);               \
+    } while (0)
+    SW_TRY(hipMalloc((void **)&d_off, (P + 1) * 4));
+    SW_TRY(hipMalloc((void **)&d_poff, (P + 1) * 4));
+    SW_TRY(hipMalloc((void **)&d_rp, (size_t(n) + 1) * 4));
+    SW_TRY(hipMemcpyAsync(d_off, off.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
+    SW_TRY(hipMemcpyAsync(d_poff, poff.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
+    SW_TRY(hipMemcpyAsync(d_rp, h_rp, (size_t(n) + 1) * 4, hipMemcpyHostToDevice, s));
+    if (nnz) {
+        SW_TRY(hipMalloc((void **)&k0, nnz * 4));
+        SW_TRY(hipMalloc((void **)&k1, nnz * 4));
+        SW_TRY(hipMalloc((void **)&i0, nnz * 4));
+        SW_TRY(hipMalloc((void **)&i1, nnz * 4));
+        hipLaunchKernelGGL(k_sweep_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_rp, d_col_src,
+                           p.d_panel_row, P, n, nbuckets, shift, k0, i0);
+        SW_TRY(hipGetLastError());
+        SW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, i0, i1, (int)nnz, 0, end_bit, s));
+        SW_TRY(hipMalloc(&tmp, tmp_bytes));
+        SW_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k0, k1, i0, i1, (int)nnz, 0, end_bit, s));
+        hipLaunchKernelGGL((k_sweep_scatter<ValueType>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, k1,
+                           i1, nnz, nbuckets, d_rp, n, d_col_src, d_val_src, p.d_panel_row, d_off, d_poff,
+                           p.d_s_col, p.d_s_row, p.d_s_val);
+        SW_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL((k_sweep_pad<ValueType>), dim3((P + 255) / 256), dim3(256), 0, s, P, p.d_panel_row, d_off,
+                       d_poff, p.d_s_col, p.d_s_row, p.d_s_val);
+    SW_TRY(hipGetLastError());
+    SW_TRY(hipStreamSynchronize(s));
+#undef SW_TRY
+    cleanup();
+    return 0;
+}
+
+// fraction of sampled rows (with >= 2 entries) whose first two columns lie < 64 apart
+int probe_locality(const IndexType *d_rp, const IndexType *d_col, IndexType n, hipStream_t s, double *frac)
+{
+    *frac = 1.0;
+    if (n == 0)
+        return 0;
+    unsigned long long *d_cnt = nullptr, h[2] = {0, 0};
+    SPMV_TRY(hipMalloc((void **)&d_cnt, 16));
+    SPMV_TRY(hipMemsetAsync(d_cnt, 0, 16, s));
+    const uint32_t stride = std::max<uint32_t>(1, n / 65536);
+    const uint64_t threads = (n + stride - 1) / stride;
+    hipLaunchKernelGGL(k_locality, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, d_rp, d_col, n, stride,
+                       d_cnt);
+    SPMV_TRY(hipGetLastError());
+    SPMV_TRY(hipMemcpyAsync(h, d_cnt, 16, hipMemcpyDeviceToHost, s));
+    SPMV_TRY(hipStreamSynchronize(s));
+    SPMV_TRY(hipFree(d_cnt));
+    *frac = h[0] ? double(h[1]) / double(h[0]) : 1.0;
+    return 0;
+}
+
+}  // namespace spmvhw

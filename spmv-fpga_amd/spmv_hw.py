@@ -90,7 +90,7 @@ EXPORTS = [
     "storage_overhead", "verification",
     "spmv_hw_units", "spmv_hw_value_bytes", "spmv_hw_last_error",
     "spmv_plan_create_device", "spmv_plan_create_host", "spmv_plan_run", "spmv_plan_get_stats",
-    "spmv_plan_set_timing", "spmv_plan_get_timing", "spmv_plan_destroy", "spmv_partition_rows",
+    "spmv_plan_set_variant", "spmv_plan_set_timing", "spmv_plan_get_timing", "spmv_plan_destroy", "spmv_partition_rows",
     "spmv_gen_banded", "spmv_gen_powerlaw_row_ptr", "spmv_gen_fill", "spmv_gen_vector",
 ]
 
@@ -132,6 +132,7 @@ class Lib:
             "spmv_plan_run": (ctypes.c_int, [vp, vp, vp, vp]),
             "spmv_plan_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(spmv_plan_stats)]),
             "spmv_plan_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+            "spmv_plan_set_variant": (ctypes.c_int, [vp, ctypes.c_int]),
             "spmv_plan_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
             "spmv_plan_destroy": (None, [vp]),
@@ -278,6 +279,9 @@ class Plan:
         st = spmv_plan_stats()
         self.lib._ok(self.lib.L.spmv_plan_get_stats(self.h, ctypes.byref(st)), "spmv_plan_get_stats")
         return st.as_dict()
+
+    def set_variant(self, variant: int) -> None:
+        self.lib._ok(self.lib.L.spmv_plan_set_variant(self.h, int(variant)), "spmv_plan_set_variant")
 
     def set_timing(self, on: bool) -> None:
         self.lib._ok(self.lib.L.spmv_plan_set_timing(self.h, int(on)), "spmv_plan_set_timing")

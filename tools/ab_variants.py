@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of kernel variants on one plan, in one process (methodology rule 24 of
+cdna_hip_programming.md §5.4): N variants x M rounds, median and min of the main kernel's HIP-event
+duration. Prints one JSON line per workload."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "spmv-fpga_amd"))
+import torch  # noqa: E402
+
+import spmv_hw  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="powerlaw,banded")
+    ap.add_argument("--dtype", default="f64")
+    ap.add_argument("--variants", default="tiles:0,tiles:1,sweep:0",
+                    help="comma list of kernel:variant (kernel = tiles | sweep)")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--nnz", type=int, default=None)
+    a = ap.parse_args()
+    dtype = np.float64 if a.dtype == "f64" else np.float32
+    lib = spmv_hw.load(dtype)
+    variants = [v if ":" in v else f"tiles:{v}" for v in a.variants.split(",")]
+    for wl in a.workload.split(","):
+        if wl == "banded":
+            n = a.rows or 1_000_000
+            rp, col, val = spmv_hw.gen_banded(lib, n, 16)
+            x = spmv_hw.gen_vector(lib, n, seed=3)
+        else:
+            n = a.rows or 10_000_000
+            rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, a.nnz or 16 * n)
+            x = spmv_hw.gen_vector(lib, n, seed=6)
+        plans = {}
+        for v in variants:
+            k, var = v.split(":")
+            if k not in plans:
+                os.environ["SPMV_HW_KERNEL"] = k
+                plans[k] = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+        os.environ.pop("SPMV_HW_KERNEL", None)
+        st = next(iter(plans.values())).stats()
+        del rp, col, val
+        y = torch.empty(n, dtype=x.dtype, device="cuda")
+        res = {v: [] for v in variants}
+        ref = None
+        for r in range(a.rounds):
+            for v in variants:
+                k, var = v.split(":")
+                plan = plans[k]
+                plan.set_variant(int(var))
+                plan.run(x, y)
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = y.clone()
+                else:
+                    err = float(((ref - y).abs().max() / ref.abs().max().clamp_min(1e-300)).item())
+                    assert err < 1e-9, f"{v} changed the result ({err})"
+                plan.set_timing(True)
+                for _ in range(a.reps):
+                    plan.run(x, y)
+                ms, _, _ = plan.timing()
+                plan.set_timing(False)
+                res[v].append(ms)
+        out = {"workload": wl, "dtype": a.dtype, "nnz": st["nr_nzeros"], "alg_bytes": st["algorithmic_bytes"],
+               "plans": {k: {kk: p.stats()[kk] for kk in ("kernel", "nr_tiles", "device_bytes")} for k, p in plans.items()}}
+        for v in variants:
+            med = float(np.median(res[v]))
+            out[v] = {"median_ms": round(med, 5), "min_ms": round(min(res[v]), 5),
+                      "alg_GBps": round(st["algorithmic_bytes"] / (med * 1e-3) / 1e9, 1)}
+        print(json.dumps(out), flush=True)
+        for p in plans.values():
+            p.destroy()
+
+
+if __name__ == "__main__":
+    main()

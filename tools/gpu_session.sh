@@ -22,12 +22,23 @@ run() {  # name seconds cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf -x ;;
+    tests_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench32) run bench_f32 600 python bench.py --dtype f32 --no-cpu ;;
     banded) run bench_banded 300 python bench.py --workload banded ;;
-    prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
+    calib) run calib 300 tools/hbm_calib ;;
+    ab) run ab 600 python tools/ab_variants.py ;;
+    counters) run counters 120 rocprofv3 -L ;;
+    pmc) for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+           tagc=$(echo $c | tr ' ' '_')
+           run pmc_$tagc 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$tagc" -o run -- python tools/ab_variants.py --variants tiles:0,sweep:0 --rounds 1 --reps 3
+         done ;;
+    pmc_calib) for c in FETCH_SIZE WRITE_SIZE; do
+           run pmccal_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmccal_$c" -o run -- tools/hbm_calib
+         done ;;
     *) echo "unknown step $s" ;;
   esac
 done
