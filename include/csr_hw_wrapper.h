@@ -93,8 +93,10 @@ int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *matrix
 /* d_y[0:nr_rows) = A * d_x  (overwrite; empty rows get 0). Asynchronous on `stream`. */
 int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, void *stream);
 int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
-/* Kernel variant bits (performance experiments; results are identical for every variant):
- * bit 0 = non-temporal streamed loads (default on), bit 1 = non-temporal y stores. */
+/* Kernel variant bits (performance experiments; every variant computes the same y).
+ * Tile kernel: bit 0 = non-temporal streamed loads, bit 1 = non-temporal y stores (default 0).
+ * Sweep kernel: bit 0 = non-temporal entry loads, bit 1 = workgroup barrier per iteration,
+ * bit 2 = two quads per thread per iteration (default 3). */
 int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */

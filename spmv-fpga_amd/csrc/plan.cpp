@@ -331,11 +331,14 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
 
 int spmv_plan_set_variant(spmv_plan *p, int variant)
 {
-    if (!p || variant < 0 || variant > 3) {
+    if (!p || variant < 0 || variant > 7) {
         set_error("spmv_plan_set_variant: bad arguments");
         return 1;
     }
-    p->variant = variant;
+    if (p->kernel == kKernelSweep)
+        p->sweep_variant = variant;
+    else
+        p->variant = variant & 3;
     return 0;
 }
 

@@ -52,7 +52,8 @@ struct spmv_plan {
     uint64_t ntiles = 0;
     bool has_empty = false;
     int kernel = 0;
-    int variant = 1;           // kernel variant bits (spmv_plan_set_variant)
+    int variant = 0;           // tile-kernel variant bits (spmv_plan_set_variant)
+    int sweep_variant = 3;     // sweep-kernel variant bits (spmv_plan_set_variant, kernel 2)
 
     uint32_t *d_col = nullptr;
     ValueType *d_val = nullptr;

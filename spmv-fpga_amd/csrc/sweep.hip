@@ -30,19 +30,32 @@ typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+template <bool NT, typename T>
+__device__ __forceinline__ T lds_(const T *p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+template <bool NT>
 __device__ __forceinline__ void load4(const double *__restrict__ v, uint64_t e, double (&o)[4])
 {
-    const f64x2 a = *reinterpret_cast<const f64x2 *>(v + e);
-    const f64x2 b = *reinterpret_cast<const f64x2 *>(v + e + 2);
+    const f64x2 a = lds_<NT>(reinterpret_cast<const f64x2 *>(v + e));
+    const f64x2 b = lds_<NT>(reinterpret_cast<const f64x2 *>(v + e + 2));
     o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
 }
+template <bool NT>
 __device__ __forceinline__ void load4(const float *__restrict__ v, uint64_t e, float (&o)[4])
 {
-    const f32x4 a = *reinterpret_cast<const f32x4 *>(v + e);
+    const f32x4 a = lds_<NT>(reinterpret_cast<const f32x4 *>(v + e));
     o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
 }
 
-template <typename V>
+// Q quads (4 entries each) per thread per workgroup iteration; SYNC: barrier after every
+// iteration so the 16 waves stay on the same column window; NT: non-temporal entry loads.
+template <typename V, int Q, bool SYNC, bool NT>
 __global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
@@ -56,37 +69,34 @@ __global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
     for (uint32_t i = threadIdx.x; i <= R; i += kSweepThreads)
         ylds[i] = V(0);
     __syncthreads();
-    constexpr uint64_t kStride = 4ull * kSweepThreads;
-    uint64_t e = e0 + 4ull * threadIdx.x;
-    // two quads per thread per iteration: 8 gathers in flight
-    for (; e + kStride < e1; e += 2 * kStride) {
-        const u32x4 ca = *reinterpret_cast<const u32x4 *>(col + e);
-        const u32x4 cb = *reinterpret_cast<const u32x4 *>(col + e + kStride);
-        const u16x4 ra = *reinterpret_cast<const u16x4 *>(row + e);
-        const u16x4 rb = *reinterpret_cast<const u16x4 *>(row + e + kStride);
-        V va[4], vb[4];
-        load4(val, e, va);
-        load4(val, e + kStride, vb);
-        const V xa0 = x[ca.x], xa1 = x[ca.y], xa2 = x[ca.z], xa3 = x[ca.w];
-        const V xb0 = x[cb.x], xb1 = x[cb.y], xb2 = x[cb.z], xb3 = x[cb.w];
-        atomicAdd(&ylds[ra.x], va[0] * xa0);
-        atomicAdd(&ylds[ra.y], va[1] * xa1);
-        atomicAdd(&ylds[ra.z], va[2] * xa2);
-        atomicAdd(&ylds[ra.w], va[3] * xa3);
-        atomicAdd(&ylds[rb.x], vb[0] * xb0);
-        atomicAdd(&ylds[rb.y], vb[1] * xb1);
-        atomicAdd(&ylds[rb.z], vb[2] * xb2);
-        atomicAdd(&ylds[rb.w], vb[3] * xb3);
-    }
-    if (e < e1) {
-        const u32x4 ca = *reinterpret_cast<const u32x4 *>(col + e);
-        const u16x4 ra = *reinterpret_cast<const u16x4 *>(row + e);
-        V va[4];
-        load4(val, e, va);
-        atomicAdd(&ylds[ra.x], va[0] * x[ca.x]);
-        atomicAdd(&ylds[ra.y], va[1] * x[ca.y]);
-        atomicAdd(&ylds[ra.z], va[2] * x[ca.z]);
-        atomicAdd(&ylds[ra.w], va[3] * x[ca.w]);
+    constexpr uint64_t kQuad = 4ull * kSweepThreads;  // entries per quad sweep of the workgroup
+    for (uint64_t base = e0; base < e1; base += Q * kQuad) {
+        u32x4 c[Q];
+        u16x4 r[Q];
+        V v[Q][4];
+        bool ok[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint64_t e = base + q * kQuad + 4ull * threadIdx.x;
+            ok[q] = e < e1;
+            if (ok[q]) {
+                c[q] = lds_<NT>(reinterpret_cast<const u32x4 *>(col + e));
+                r[q] = lds_<NT>(reinterpret_cast<const u16x4 *>(row + e));
+                load4<NT>(val, e, v[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (ok[q]) {
+                const V x0 = x[c[q].x], x1 = x[c[q].y], x2 = x[c[q].z], x3 = x[c[q].w];
+                atomicAdd(&ylds[r[q].x], v[q][0] * x0);
+                atomicAdd(&ylds[r[q].y], v[q][1] * x1);
+                atomicAdd(&ylds[r[q].z], v[q][2] * x2);
+                atomicAdd(&ylds[r[q].w], v[q][3] * x3);
+            }
+        }
+        if constexpr (SYNC)
+            __syncthreads();
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < R; i += kSweepThreads)
@@ -186,8 +196,22 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
     if (p.npanels == 0)
         return hipSuccess;
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(ValueType);
-    hipLaunchKernelGGL((k_spmv_sweep<ValueType>), dim3((unsigned)p.npanels), dim3(kSweepThreads), lds, s,
-                       p.d_s_col, p.d_s_row, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+    // variant bits: 0 = non-temporal entry loads, 1 = barrier per iteration, 2 = two quads/iteration
+#define SWEEP(Q, SYNC, NT)                                                                        \
+    hipLaunchKernelGGL((k_spmv_sweep<ValueType, Q, SYNC, NT>), dim3((unsigned)p.npanels),            \
+                       dim3(kSweepThreads), lds, s, p.d_s_col, p.d_s_row, p.d_s_val, p.d_panel_row, \
+                       p.d_panel_ent, d_x, d_y)
+    switch (p.sweep_variant & 7) {
+    case 0: SWEEP(1, false, false); break;
+    case 1: SWEEP(1, false, true); break;
+    case 2: SWEEP(1, true, false); break;
+    case 3: SWEEP(1, true, true); break;
+    case 4: SWEEP(2, false, false); break;
+    case 5: SWEEP(2, false, true); break;
+    case 6: SWEEP(2, true, false); break;
+    default: SWEEP(2, true, true); break;
+    }
+#undef SWEEP
     return hipGetLastError();
 }
 

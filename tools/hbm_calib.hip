@@ -67,6 +67,33 @@ __global__ void k_gather(const double *__restrict__ t, size_t tn, size_t per_thr
         sink[0] = acc;
 }
 
+// the same L2-resident gather with other load flavours: 1 = sc1 (L1 bypass), 2 = nt
+template <int KIND>
+__global__ void k_gather_kind(const double *__restrict__ t, size_t tn, size_t per_thread, double *__restrict__ sink)
+{
+    const size_t tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    double acc = 0.0;
+    for (size_t it = 0; it < per_thread; it += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const double *p = t + mix(tid * 0x10000ull + it + j) % tn;
+            if constexpr (KIND == 1)
+                v[j] = __builtin_bit_cast(double, __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT));
+            else if constexpr (KIND == 2)
+                v[j] = __builtin_nontemporal_load(p);
+            else
+                v[j] = *p;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            acc += v[j];
+    }
+    if (acc == 1.2345)
+        sink[0] = acc;
+}
+
 // gathers confined to a window that sweeps the table (the column-sorted "x sweep" pattern):
 // iteration `it` of every thread reads inside [it*step, it*step + win) mod tn
 __global__ void k_gather_sweep(const double *__restrict__ t, size_t tn, size_t per_thread, size_t win,
@@ -173,6 +200,21 @@ int main()
                 hipLaunchKernelGGL(k_gather, dim3(grid), dim3(block), 0, 0, (const double *)a, kb * 1024 / 8,
                                    per_thread, sink);
             }, nreq * 8, nreq))
+            return 1;
+    }
+    for (int kind = 0; kind < 3; ++kind) {
+        char name[64];
+        std::snprintf(name, sizeof name, "gather_2MB_kind%d", kind);
+        auto go = [&] {
+            const size_t tn = 2048 * 1024 / 8;
+            if (kind == 0)
+                hipLaunchKernelGGL(k_gather_kind<0>, dim3(grid), dim3(block), 0, 0, (const double *)a, tn, per_thread, sink);
+            else if (kind == 1)
+                hipLaunchKernelGGL(k_gather_kind<1>, dim3(grid), dim3(block), 0, 0, (const double *)a, tn, per_thread, sink);
+            else
+                hipLaunchKernelGGL(k_gather_kind<2>, dim3(grid), dim3(block), 0, 0, (const double *)a, tn, per_thread, sink);
+        };
+        if (timed(name, go, nreq * 8, nreq))
             return 1;
     }
     for (size_t win : {8192ull, 65536ull, 262144ull}) {
