@@ -53,14 +53,39 @@ __device__ __forceinline__ void load4(const float *__restrict__ v, uint64_t e, f
     o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
 }
 
-// Q quads (4 entries each) per thread per workgroup iteration; SYNC: barrier after every
-// iteration so the 16 waves stay on the same column window; NT: non-temporal entry loads.
-template <typename V, int Q, bool SYNC, bool NT>
+template <int E> struct EntryVec;
+template <> struct EntryVec<4> { typedef u32x4 C; typedef u16x4 R; };
+template <> struct EntryVec<2> {
+    typedef uint32_t C __attribute__((ext_vector_type(2)));
+    typedef uint16_t R __attribute__((ext_vector_type(2)));
+};
+
+template <bool NT, int E, typename V>
+__device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o)[E])
+{
+    if constexpr (E == 4) {
+        load4<NT>(v, e, o);
+    } else if constexpr (sizeof(V) == 8) {
+        const f64x2 a = lds_<NT>(reinterpret_cast<const f64x2 *>(v + e));
+        o[0] = a.x; o[1] = a.y;
+    } else {
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 a = lds_<NT>(reinterpret_cast<const f32x2 *>(v + e));
+        o[0] = a.x; o[1] = a.y;
+    }
+}
+
+// E entries per thread per workgroup iteration, Q such groups per iteration; SYNC: barrier after
+// every iteration so the 16 waves stay on one column window; NT: non-temporal entry loads.
+// Entry ranges of a panel are multiples of 4, so whole E-groups are always valid.
+template <typename V, int E, int Q, bool SYNC, bool NT>
 __global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
     const V *__restrict__ x, V *__restrict__ y)
 {
+    typedef typename EntryVec<E>::C CV;
+    typedef typename EntryVec<E>::R RV;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     V *ylds = reinterpret_cast<V *>(smem);
     const uint32_t p = blockIdx.x;
@@ -69,30 +94,32 @@ __global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
     for (uint32_t i = threadIdx.x; i <= R; i += kSweepThreads)
         ylds[i] = V(0);
     __syncthreads();
-    constexpr uint64_t kQuad = 4ull * kSweepThreads;  // entries per quad sweep of the workgroup
-    for (uint64_t base = e0; base < e1; base += Q * kQuad) {
-        u32x4 c[Q];
-        u16x4 r[Q];
-        V v[Q][4];
+    constexpr uint64_t kGroup = (uint64_t)E * kSweepThreads;  // entries per workgroup group
+    for (uint64_t base = e0; base < e1; base += Q * kGroup) {
+        CV c[Q];
+        RV r[Q];
+        V v[Q][E];
         bool ok[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const uint64_t e = base + q * kQuad + 4ull * threadIdx.x;
+            const uint64_t e = base + q * kGroup + (uint64_t)E * threadIdx.x;
             ok[q] = e < e1;
             if (ok[q]) {
-                c[q] = lds_<NT>(reinterpret_cast<const u32x4 *>(col + e));
-                r[q] = lds_<NT>(reinterpret_cast<const u16x4 *>(row + e));
-                load4<NT>(val, e, v[q]);
+                c[q] = lds_<NT>(reinterpret_cast<const CV *>(col + e));
+                r[q] = lds_<NT>(reinterpret_cast<const RV *>(row + e));
+                loadv<NT, E>(val, e, v[q]);
             }
         }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if (ok[q]) {
-                const V x0 = x[c[q].x], x1 = x[c[q].y], x2 = x[c[q].z], x3 = x[c[q].w];
-                atomicAdd(&ylds[r[q].x], v[q][0] * x0);
-                atomicAdd(&ylds[r[q].y], v[q][1] * x1);
-                atomicAdd(&ylds[r[q].z], v[q][2] * x2);
-                atomicAdd(&ylds[r[q].w], v[q][3] * x3);
+                V xv[E];
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    xv[j] = x[c[q][j]];
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    atomicAdd(&ylds[r[q][j]], v[q][j] * xv[j]);
             }
         }
         if constexpr (SYNC)
@@ -196,20 +223,26 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
     if (p.npanels == 0)
         return hipSuccess;
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(ValueType);
-    // variant bits: 0 = non-temporal entry loads, 1 = barrier per iteration, 2 = two quads/iteration
-#define SWEEP(Q, SYNC, NT)                                                                        \
-    hipLaunchKernelGGL((k_spmv_sweep<ValueType, Q, SYNC, NT>), dim3((unsigned)p.npanels),            \
+    // variant bits: 0 = non-temporal entry loads, 1 = barrier per iteration,
+    // 2 = two groups per iteration, 3 = groups of 2 entries per thread (default 4)
+#define SWEEP(E, Q, SYNC, NT)                                                                     \
+    hipLaunchKernelGGL((k_spmv_sweep<ValueType, E, Q, SYNC, NT>), dim3((unsigned)p.npanels),         \
                        dim3(kSweepThreads), lds, s, p.d_s_col, p.d_s_row, p.d_s_val, p.d_panel_row, \
                        p.d_panel_ent, d_x, d_y)
-    switch (p.sweep_variant & 7) {
-    case 0: SWEEP(1, false, false); break;
-    case 1: SWEEP(1, false, true); break;
-    case 2: SWEEP(1, true, false); break;
-    case 3: SWEEP(1, true, true); break;
-    case 4: SWEEP(2, false, false); break;
-    case 5: SWEEP(2, false, true); break;
-    case 6: SWEEP(2, true, false); break;
-    default: SWEEP(2, true, true); break;
+    switch (p.sweep_variant & 15) {
+    case 0: SWEEP(4, 1, false, false); break;
+    case 1: SWEEP(4, 1, false, true); break;
+    case 2: SWEEP(4, 1, true, false); break;
+    case 3: SWEEP(4, 1, true, true); break;
+    case 4: SWEEP(4, 2, false, false); break;
+    case 5: SWEEP(4, 2, false, true); break;
+    case 6: SWEEP(4, 2, true, false); break;
+    case 7: SWEEP(4, 2, true, true); break;
+    case 10: SWEEP(2, 1, true, false); break;
+    case 11: SWEEP(2, 1, true, true); break;
+    case 14: SWEEP(2, 2, true, false); break;
+    case 15: SWEEP(2, 2, true, true); break;
+    default: SWEEP(4, 1, true, true); break;
     }
 #undef SWEEP
     return hipGetLastError();

@@ -31,11 +31,11 @@ for s in $STEPS; do
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
     calib) run calib 300 tools/hbm_calib ;;
     ab) run ab 600 python tools/ab_variants.py ;;
-    absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants tiles:0,sweep:0,sweep:1,sweep:2,sweep:3,sweep:4,sweep:5,sweep:6,sweep:7 ;;
+    absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants tiles:0,sweep:2,sweep:3,sweep:7,sweep:10,sweep:11,sweep:14,sweep:15 ;;
     counters) run counters 120 rocprofv3 -L ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
            tagc=$(echo $c | tr ' ' '_')
-           run pmc_$tagc 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$tagc" -o run -- python tools/ab_variants.py --workload powerlaw --variants sweep:2,sweep:3 --rounds 1 --reps 3
+           run pmc_$tagc 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$tagc" -o run -- python tools/ab_variants.py --workload powerlaw --variants sweep:3,sweep:11 --rounds 1 --reps 3
          done ;;
     pmc_calib) for c in FETCH_SIZE WRITE_SIZE; do
            run pmccal_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmccal_$c" -o run -- tools/hbm_calib
