@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     const uint32_t *__restrict__ col, const V *__restrict__ val, const uint32_t *__restrict__ rowend,
     const uint32_t *__restrict__ tile_info, const uint32_t *__restrict__ row_id,
     const V *__restrict__ x, V *__restrict__ y, V *__restrict__ head, V *__restrict__ tail,
-    uint8_t *__restrict__ tflags, uint64_t nnz, uint64_t ntiles)
+    uint64_t nnz, uint64_t ntiles)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t t = (uint64_t)blockIdx.x * (kBlockThreads / kWave) + (threadIdx.x >> 6);
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     const uint32_t info = tile_info[t];
     uint32_t rowc = info >> 1;          // compact row of the tile's first entry
     bool pending = (info & 1u) != 0;    // first row end of the tile closes a row begun earlier
-    bool any_end = false, last_is_end = false;
+    bool last_is_end = false;
     V carry = V(0);
 
 #pragma unroll
@@ -174,48 +174,32 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
         const int F63 = __shfl(F, kWave - 1, kWave);
         carry = F63 ? I63 : carry + I63;
         rowc += (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
-        if (bany) {
+        if (bany)
             pending = false;
-            any_end = true;
-        }
         last_is_end = (b3 >> 63) & 1ull;
     }
 
-    if (lane == 0) {
-        const bool has_tail = !last_is_end && (k0 + (uint64_t)(U * kStep) < nnz);
-        if (has_tail)
-            tail[t] = carry;
-        tflags[t] = (uint8_t)((has_tail ? kHasTail : 0) | (any_end ? kHasEnd : 0));
-    }
+    if (lane == 0 && !last_is_end && (k0 + (uint64_t)(U * kStep) < nnz))
+        tail[t] = carry;  // the tile ends inside a row that continues in tile t+1
 }
 
-// Completes rows that cross tile boundaries: partials are added in tile order.
+// Completes every row that crosses a tile boundary. The crossings are structural (known when
+// the plan is built): crossing c covers tiles [first, last]; its sum is tail[first] + tail[first+1]
+// + ... + tail[last-1] + head[last], added in tile order (deterministic, no atomics).
 template <typename V>
-__global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ tflags,
+__global__ __launch_bounds__(256) void k_fixup(const uint32_t *__restrict__ cross, uint64_t ncross,
                                                const V *__restrict__ head, const V *__restrict__ tail,
-                                               const uint32_t *__restrict__ tile_info,
-                                               const uint32_t *__restrict__ row_id, V *__restrict__ y,
-                                               uint64_t ntiles)
+                                               const uint32_t *__restrict__ row_id, V *__restrict__ y)
 {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles)
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncross)
         return;
-    const uint8_t f = tflags[t];
-    if (!(f & kHasTail))
-        return;
-    if (!(f & kHasEnd) && t > 0 && (tflags[t - 1] & kHasTail))
-        return;  // a middle tile: the row began in an earlier tile
-    V acc = tail[t];
-    uint64_t j = t + 1;
-    while (j < ntiles && !(tflags[j] & kHasEnd)) {
+    const uint32_t row = cross[3 * c], first = cross[3 * c + 1], last = cross[3 * c + 2];
+    V acc = tail[first];
+    for (uint32_t j = first + 1; j < last; ++j)
         acc = acc + tail[j];
-        ++j;
-    }
-    if (j >= ntiles)
-        return;  // unreachable for a well-formed plan (the last stored entry ends a row)
-    acc = acc + head[j];
-    const uint32_t r = tile_info[t + 1] >> 1;
-    y[row_id ? row_id[r] : r] = acc;
+    acc = acc + head[last];
+    y[row_id ? row_id[row] : row] = acc;
 }
 
 // Copies logical CSR col/val into the padded hw representation (fp64: pair-interleaved).
@@ -251,7 +235,7 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
 #define SPMV_LAUNCH(VAR)                                                                          \
     hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps, VAR>), dim3((unsigned)blocks),         \
                        dim3(kBlockThreads), 0, s, p.d_col, p.d_val, p.d_rowend, p.d_tile_info,      \
-                       p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.d_tflags, p.nnz, p.ntiles)
+                       p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.nnz, p.ntiles)
     switch (p.variant & 3) {
     case 0: SPMV_LAUNCH(0); break;
     case 1: SPMV_LAUNCH(1); break;
@@ -264,11 +248,11 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
 
 hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s)
 {
-    if (p.ntiles < 2)
+    if (p.ncross == 0)
         return hipSuccess;
-    const uint64_t blocks = (p.ntiles + 255) / 256;
-    hipLaunchKernelGGL((k_fixup<ValueType>), dim3((unsigned)blocks), dim3(256), 0, s, p.d_tflags,
-                       p.d_head, p.d_tail, p.d_tile_info, p.d_row_id, d_y, p.ntiles);
+    const uint64_t blocks = (p.ncross + 255) / 256;
+    hipLaunchKernelGGL((k_fixup<ValueType>), dim3((unsigned)blocks), dim3(256), 0, s, p.d_cross, p.ncross,
+                       p.d_head, p.d_tail, p.d_row_id, d_y);
     return hipGetLastError();
 }
 

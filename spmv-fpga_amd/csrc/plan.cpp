@@ -73,6 +73,36 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
             tile_info[t] = (uint32_t)(c << 1) | (cont ? 1u : 0u);
         }
     }
+    // rows crossing tile boundaries (structural): tile t "has a tail" when its last entry is not
+    // a row end and entries follow; a crossing starts at a tile with a tail whose row began in
+    // it, and ends at the next tile that contains a row end
+    std::vector<uint32_t> cross;
+    {
+        auto bit = [&](uint64_t k) { return (rowend[k >> 5] >> (k & 31)) & 1u; };
+        std::vector<uint8_t> has_tail(p.ntiles, 0), has_end(p.ntiles, 0);
+        for (uint64_t t = 0; t < p.ntiles; ++t) {
+            const uint64_t w0 = t * (kTileNnz / 32);
+            for (uint64_t w = 0; w < kTileNnz / 32; ++w)
+                has_end[t] |= rowend[w0 + w] != 0;
+            const uint64_t last = (t + 1) * kTileNnz - 1;
+            has_tail[t] = (last + 1 < nnz) && !bit(last);
+        }
+        for (uint64_t t = 0; t < p.ntiles; ++t) {
+            if (!has_tail[t] || !(has_end[t] || t == 0 || !has_tail[t - 1]))
+                continue;
+            uint64_t j = t + 1;
+            while (j < p.ntiles && !has_end[j])
+                ++j;
+            if (j >= p.ntiles) {
+                set_error("internal: unterminated row crossing");
+                return 1;
+            }
+            cross.push_back(tile_info[t + 1] >> 1);
+            cross.push_back((uint32_t)t);
+            cross.push_back((uint32_t)j);
+        }
+        p.ncross = cross.size() / 3;
+    }
     auto alloc = [&](void **ptr, size_t bytes) -> hipError_t {
         *ptr = nullptr;
         return bytes ? hipMalloc(ptr, bytes) : hipSuccess;
@@ -83,7 +113,7 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
     SPMV_TRY(alloc((void **)&p.d_tile_info, tile_info.size() * sizeof(uint32_t)));
     SPMV_TRY(alloc((void **)&p.d_head, p.ntiles * sizeof(ValueType)));
     SPMV_TRY(alloc((void **)&p.d_tail, p.ntiles * sizeof(ValueType)));
-    SPMV_TRY(alloc((void **)&p.d_tflags, p.ntiles));
+    SPMV_TRY(alloc((void **)&p.d_cross, cross.size() * sizeof(uint32_t)));
     if (p.has_empty)
         SPMV_TRY(alloc((void **)&p.d_row_id, row_id.size() * sizeof(uint32_t)));
     if (!rowend.empty())
@@ -91,6 +121,8 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
     SPMV_TRY(hipMemcpyAsync(p.d_tile_info, tile_info.data(), tile_info.size() * 4, hipMemcpyHostToDevice, s));
     if (p.has_empty && !row_id.empty())
         SPMV_TRY(hipMemcpyAsync(p.d_row_id, row_id.data(), row_id.size() * 4, hipMemcpyHostToDevice, s));
+    if (!cross.empty())
+        SPMV_TRY(hipMemcpyAsync(p.d_cross, cross.data(), cross.size() * 4, hipMemcpyHostToDevice, s));
     if (p.nnz_pad)
         SPMV_TRY(launch_pack(d_col_src, d_val_src, nnz, p.nnz_pad, p.nr_cols, p.d_col, p.d_val, nullptr, s));
     // pageable host vectors above go out of scope: make the copies complete first
@@ -195,7 +227,7 @@ spmv_plan::~spmv_plan()
     (void)hipSetDevice(device);
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
-                      (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_tflags, (void *)d_s_col,
+                      (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
                       (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_panel_ent})
         if (ptr)
             (void)hipFree(ptr);
@@ -208,7 +240,7 @@ uint64_t spmv_plan::device_bytes() const
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + sizeof(uint16_t) + sizeof(ValueType)) + (npanels + 1) * 8;
     return nnz_pad * (sizeof(uint32_t) + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
-           (has_empty ? nzr * 4 : 0) + ntiles * (2 * sizeof(ValueType) + 1);
+           (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;
 }
 
 // z*(sizeof(val)+4) + (n+1)*4 + m*sizeof(val) + n*sizeof(val)

@@ -39,9 +39,6 @@ constexpr uint64_t kSweepLdsBytes = 160 * 1024;    // LDS of one CU holds the pa
 constexpr int kKernelTiles = 0;  // flagged-tile wave kernel, x gathered through the caches
 constexpr int kKernelSweep = 2;  // panel sweep: y in LDS, columns swept in order (x from L2)
 
-// tile flags written by the main kernel, read by the fix-up kernel
-constexpr uint8_t kHasTail = 1;   // tile ends inside a row that continues in the next tile
-constexpr uint8_t kHasEnd = 2;    // tile contains at least one row end
 }  // namespace spmvhw
 
 struct spmv_plan {
@@ -62,7 +59,8 @@ struct spmv_plan {
     uint32_t *d_row_id = nullptr;
     ValueType *d_head = nullptr;
     ValueType *d_tail = nullptr;
-    uint8_t *d_tflags = nullptr;
+    uint32_t *d_cross = nullptr;   // rows crossing tile boundaries: (row, first tile, last tile)
+    uint64_t ncross = 0;
 
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
