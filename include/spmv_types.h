@@ -13,6 +13,10 @@
  *
  * Build knob: DOUBLE=1 (default) -> ValueType double, DOUBLE=0 -> float, exactly as the
  * reference's Makefile:17,71 passes -DDOUBLE. One shared library is built per precision.
+ *
+ * Drop-in use from the reference's own sources: include the reference's util.h and csr.h first
+ * and define SPMV_USE_CALLER_CSR_TYPES; the caller's IndexType/ValueType/csr_* types and its
+ * ap_uint<128> BusDataType are then used (same sizes and field order), see INTEGRATION.md §1.
  */
 #ifndef SPMV_TYPES_H
 #define SPMV_TYPES_H
@@ -24,25 +28,36 @@
 #define DOUBLE 1
 #endif
 
+#ifndef SPMV_USE_CALLER_CSR_TYPES
 typedef uint32_t IndexType;               /* util.h:9  (ap_uint<32>) */
-#define INDEX_TYPE_BIT_WIDTH 32
-
 #if DOUBLE == 0
 typedef float ValueType;                  /* util.h:19 */
-#define VALUE_TYPE_BIT_WIDTH 32
 #else
 typedef double ValueType;                 /* util.h:23 */
-#define VALUE_TYPE_BIT_WIDTH 64
 #endif
-
 /* util.h:61-69: the reference moves 128-bit words over the AXI bus. On MI355X the hw
  * representation lives in HBM; a BusDataType* in the structs below is an opaque device
  * address of a 16-byte-aligned buffer. */
-#define BUS_BIT_WIDTH 128
 typedef struct BusDataType {
     uint64_t lo, hi;
 } BusDataType;
+#endif
 
+#ifndef INDEX_TYPE_BIT_WIDTH
+#define INDEX_TYPE_BIT_WIDTH 32
+#endif
+#ifndef VALUE_TYPE_BIT_WIDTH
+#if DOUBLE == 0
+#define VALUE_TYPE_BIT_WIDTH 32
+#else
+#define VALUE_TYPE_BIT_WIDTH 64
+#endif
+#endif
+#ifndef BUS_BIT_WIDTH
+#define BUS_BIT_WIDTH 128
+#endif
+
+#ifndef SPMV_USE_CALLER_CSR_TYPES
 /* csr.h:7-13 */
 typedef struct csr_header {
     IndexType nr_rows;
@@ -67,6 +82,7 @@ typedef struct csr_vector {
     ValueType *values;
     IndexType nr_values;
 } csr_vector;
+#endif /* SPMV_USE_CALLER_CSR_TYPES */
 
 /* csr_hw.h:8-14 */
 typedef struct csr_hw_header {

@@ -123,3 +123,49 @@ def test_storage_overhead_uses_64bit_sums():
     mb = lib.storage_overhead(ctypes.pointer(m))
     expect = (5 * 32 + 120_000_000 * 128) / (8.0 * 1024 * 1024)
     assert mb == pytest.approx(expect, rel=1e-12)
+
+
+DROPIN_TU = r"""
+// Stand-in for the reference's util.h/csr.h as a caller would have them: a class-typed
+// IndexType of ap_uint<32>'s size and the csr_* structs in the reference's field order.
+#include <cstdint>
+#include <cstdio>
+struct IndexType { uint32_t v; IndexType() = default; IndexType(uint32_t x) : v(x) {} operator uint32_t() const { return v; } };
+typedef double ValueType;
+struct BusDataType { uint64_t w[2]; };
+#define INDEX_TYPE_BIT_WIDTH 32
+#define VALUE_TYPE_BIT_WIDTH 64
+#define BUS_BIT_WIDTH 128
+typedef struct csr_header { IndexType nr_rows, nr_cols, nr_nzeros; int blocks; } csr_header;
+typedef struct csr_matrix { IndexType *row_ptr; IndexType *col_ind; ValueType *values;
+                            IndexType nr_nzeros, nr_rows, nr_cols; char *Filename; } csr_matrix;
+typedef struct csr_vector { ValueType *values; IndexType nr_values; } csr_vector;
+// --- the replacement src/csr_hw_wrapper.h of INTEGRATION.md ---
+#define SPMV_USE_CALLER_CSR_TYPES
+#include "spmv_mi355x.h"
+static_assert(sizeof(IndexType) == 4, "ap_uint<32> layout");
+int main() {
+    csr_matrix m{}; csr_hw_matrix **hw = nullptr; bool **bm = nullptr; csr_hw_vector *hx = nullptr;
+    csr_vector x{}, y{};
+    if (std::getenv("RUN")) {   // never executed in the CPU test: linking is what is checked
+        create_csr_hw_matrix(&m, &hw, &bm);
+        create_csr_hw_x_vector(&hx, &x, hw[0]->blocks, hw[0]->nr_cols);
+        spmv_hw(hw, hx, &y, bm);
+        std::printf("%d %f\n", verification(y.nr_values, y.values, y.values, 0), (double)storage_overhead(hw[0]));
+        delete_csr_hw_matrix(hw); std::free(bm); delete_csr_hw_x_vector(hx);
+    }
+    return 0;
+}
+"""
+
+
+def test_dropin_header_compiles_and_links_against_caller_types(tmp_path):
+    """the reference's sources keep their own csr_* types (class-typed
+    IndexType) and link the C-ABI library by name."""
+    src = tmp_path / "dropin.cpp"
+    src.write_text("#include <cstdlib>\n" + DROPIN_TU)
+    exe = tmp_path / "dropin"
+    lib_dir = os.path.dirname(spmv_hw.lib_path(np.float64))
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-o", str(exe), "-L", lib_dir, "-lspmv_hw_f64", f"-Wl,-rpath,{lib_dir}"], check=True)
+    assert exe.exists()
