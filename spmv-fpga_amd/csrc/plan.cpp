@@ -206,6 +206,11 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         }
     }
     p->kernel = kernel;
+    if (const char *t = std::getenv("SPMV_SWEEP_THREADS")) {
+        const int v = std::atoi(t);
+        if (v == 256 || v == 512 || v == 1024)
+            p->sweep_threads = v;
+    }
     if (kernel == kKernelSweep) {
         if (build_sweep(*p, h_row_ptr, d_col, d_val, s))
             return 1;
@@ -363,7 +368,7 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
 
 int spmv_plan_set_variant(spmv_plan *p, int variant)
 {
-    if (!p || variant < 0 || variant > 15) {
+    if (!p || variant < 0 || variant > 31) {
         set_error("spmv_plan_set_variant: bad arguments");
         return 1;
     }

@@ -32,7 +32,7 @@ constexpr int kStep = kWave * kLaneEntries;        // 256 entries per wave step
 constexpr int kTileSteps = 2;                      // wave steps per tile
 constexpr int kTileNnz = kStep * kTileSteps;       // 512 entries per wave tile
 constexpr int kBlockThreads = 256;                 // 4 waves = 4 tiles per workgroup
-constexpr int kSweepThreads = 1024;                // panel-sweep workgroup (16 waves, one per CU)
+constexpr int kSweepThreads = 1024;                // default panel-sweep workgroup (16 waves, 1/CU)
 constexpr uint64_t kSweepLdsBytes = 160 * 1024;    // LDS of one CU holds the panel's y
 
 // plan kernels (spmv_plan_stats.kernel)
@@ -65,6 +65,7 @@ struct spmv_plan {
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
     uint32_t panel_rmax = 0;
+    int sweep_threads = kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)
     uint32_t *d_s_col = nullptr;
     uint16_t *d_s_row = nullptr;
     ValueType *d_s_val = nullptr;

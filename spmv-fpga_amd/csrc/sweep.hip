@@ -78,8 +78,8 @@ __device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o
 // E entries per thread per workgroup iteration, Q such groups per iteration; SYNC: barrier after
 // every iteration so the 16 waves stay on one column window; NT: non-temporal entry loads.
 // Entry ranges of a panel are multiples of 4, so whole E-groups are always valid.
-template <typename V, int E, int Q, bool SYNC, bool NT>
-__global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
+template <typename V, int T, int E, int Q, bool SYNC, bool NT>
+__global__ __launch_bounds__(T) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
     const V *__restrict__ x, V *__restrict__ y)
@@ -91,10 +91,10 @@ __global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
     const uint32_t p = blockIdx.x;
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
-    for (uint32_t i = threadIdx.x; i <= R; i += kSweepThreads)
+    for (uint32_t i = threadIdx.x; i <= R; i += T)
         ylds[i] = V(0);
     __syncthreads();
-    constexpr uint64_t kGroup = (uint64_t)E * kSweepThreads;  // entries per workgroup group
+    constexpr uint64_t kGroup = (uint64_t)E * T;  // entries per workgroup group
     for (uint64_t base = e0; base < e1; base += Q * kGroup) {
         CV c[Q];
         RV r[Q];
@@ -126,7 +126,87 @@ __global__ __launch_bounds__(kSweepThreads) void k_spmv_sweep(
             __syncthreads();
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < R; i += kSweepThreads)
+    for (uint32_t i = threadIdx.x; i < R; i += T)
+        y[r0 + i] = ylds[i];
+}
+
+// Software-pipelined sweep: the entry stream of group g+1 is loaded while group g's gathers
+// and LDS adds run, so HBM latency is paid once per panel, not once per barrier. Two named
+// register sets (A/B, loop unrolled by two) avoid moves out of registers with loads in
+// flight; gathers are issued BEFORE the next group's loads, so waiting for them (vmcnt counts
+// in issue order) leaves the prefetch in flight. Loads are unconditional with clamped
+// addresses (entry ranges are multiples of 4); out-of-range groups skip their adds. One
+// barrier per group keeps the 16 waves on one column window.
+template <bool NT, typename V>
+struct SweepGroup {
+    u32x4 c;
+    u16x4 r;
+    V v[4];
+    __device__ __forceinline__ void load(const uint32_t *__restrict__ col, const uint16_t *__restrict__ row,
+                                         const V *__restrict__ val, uint64_t e)
+    {
+        c = lds_<NT>(reinterpret_cast<const u32x4 *>(col + e));
+        r = lds_<NT>(reinterpret_cast<const u16x4 *>(row + e));
+        load4<NT>(val, e, v);
+    }
+};
+
+template <typename V, int T, bool NT>
+__global__ __launch_bounds__(T) void k_spmv_sweep_pipe(
+    const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
+    const V *__restrict__ x, V *__restrict__ y)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    V *ylds = reinterpret_cast<V *>(smem);
+    const uint32_t p = blockIdx.x;
+    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
+    const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
+    for (uint32_t i = threadIdx.x; i <= R; i += T)
+        ylds[i] = V(0);
+    constexpr uint64_t kGroup = 4ull * T;
+    const uint64_t elast = e1 > e0 ? e1 - 4 : e0;  // clamp target: a valid quad of the panel
+    auto at = [&](uint64_t e) { return e < e1 ? e : elast; };
+    uint64_t e = e0 + 4ull * threadIdx.x;
+    SweepGroup<NT, V> A, B;
+    if (e1 > e0)
+        A.load(col, row, val, at(e));
+    __syncthreads();  // LDS zeroed before any add
+    for (uint64_t base = e0; base < e1; base += 2 * kGroup) {
+        // ---- group A (entries e) ----
+        V xa[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            xa[j] = x[A.c[j]];
+        __builtin_amdgcn_sched_barrier(0);  // keep the gathers ahead of the prefetch
+        B.load(col, row, val, at(e + kGroup));
+        {
+            const bool ok = e < e1;  // a clamped (duplicate) quad adds into the scratch slot R
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                atomicAdd(&ylds[ok ? (uint32_t)A.r[j] : R], A.v[j] * xa[j]);
+        }
+        __syncthreads();
+        if (base + kGroup >= e1)
+            break;
+        // ---- group B (entries e + kGroup) ----
+        V xb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            xb[j] = x[B.c[j]];
+        __builtin_amdgcn_sched_barrier(0);
+        A.load(col, row, val, at(e + 2 * kGroup));
+        {
+            const bool ok = e + kGroup < e1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                atomicAdd(&ylds[ok ? (uint32_t)B.r[j] : R], B.v[j] * xb[j]);
+        }
+        __syncthreads();
+        e += 2 * kGroup;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < R; i += T)
         y[r0 + i] = ylds[i];
 }
 
@@ -218,33 +298,47 @@ __global__ void k_locality(const IndexType *__restrict__ rp, const IndexType *__
         atomicAdd(&counts[1], 1ull);
 }
 
-hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+template <int T>
+static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
 {
-    if (p.npanels == 0)
-        return hipSuccess;
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(ValueType);
+    const dim3 grid((unsigned)p.npanels), block(T);
     // variant bits: 0 = non-temporal entry loads, 1 = barrier per iteration,
-    // 2 = two groups per iteration, 3 = groups of 2 entries per thread (default 4)
+    // 2 = two groups per iteration, 3 = groups of 2 entries per thread, 4 = pipelined stream
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
-    hipLaunchKernelGGL((k_spmv_sweep<ValueType, E, Q, SYNC, NT>), dim3((unsigned)p.npanels),         \
-                       dim3(kSweepThreads), lds, s, p.d_s_col, p.d_s_row, p.d_s_val, p.d_panel_row, \
-                       p.d_panel_ent, d_x, d_y)
+    hipLaunchKernelGGL((k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>), grid, block, lds, s, p.d_s_col, \
+                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y)
+    if (p.sweep_variant & 16) {
+        if (p.sweep_variant & 1)
+            hipLaunchKernelGGL((k_spmv_sweep_pipe<ValueType, T, true>), grid, block, lds, s, p.d_s_col, p.d_s_row,
+                               p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else
+            hipLaunchKernelGGL((k_spmv_sweep_pipe<ValueType, T, false>), grid, block, lds, s, p.d_s_col, p.d_s_row,
+                               p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        return;
+    }
     switch (p.sweep_variant & 15) {
     case 0: SWEEP(4, 1, false, false); break;
     case 1: SWEEP(4, 1, false, true); break;
     case 2: SWEEP(4, 1, true, false); break;
-    case 3: SWEEP(4, 1, true, true); break;
-    case 4: SWEEP(4, 2, false, false); break;
     case 5: SWEEP(4, 2, false, true); break;
-    case 6: SWEEP(4, 2, true, false); break;
     case 7: SWEEP(4, 2, true, true); break;
-    case 10: SWEEP(2, 1, true, false); break;
     case 11: SWEEP(2, 1, true, true); break;
-    case 14: SWEEP(2, 2, true, false); break;
     case 15: SWEEP(2, 2, true, true); break;
     default: SWEEP(4, 1, true, true); break;
     }
 #undef SWEEP
+}
+
+hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+{
+    if (p.npanels == 0)
+        return hipSuccess;
+    switch (p.sweep_threads) {
+    case 256: launch_sweep_t<256>(p, d_x, d_y, s); break;
+    case 512: launch_sweep_t<512>(p, d_x, d_y, s); break;
+    default: launch_sweep_t<1024>(p, d_x, d_y, s); break;
+    }
     return hipGetLastError();
 }
 
@@ -255,13 +349,16 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
 {
     const IndexType n = p.nr_rows;
     const uint64_t nnz = p.nnz;
-    const uint32_t rmax = (uint32_t)std::min<uint64_t>(kSweepLdsBytes / sizeof(ValueType) - 1, 65534);
+    // a workgroup of T threads gets T/1024 of one CU's LDS for its panel's y
+    const uint64_t lds_bytes = kSweepLdsBytes * p.sweep_threads / 1024;
+    const uint32_t rmax = (uint32_t)std::min<uint64_t>(lds_bytes / sizeof(ValueType) - 1, 65534);
     int cus = 256;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, p.device) == hipSuccess && prop.multiProcessorCount > 0)
             cus = prop.multiProcessorCount;
     }
+    cus *= 1024 / p.sweep_threads;  // resident workgroups per round
     std::vector<uint32_t> prow;
     for (uint64_t P = std::max<uint64_t>(1, (n + rmax - 1) / rmax);; ++P) {
         if (P > 1 && P % cus)

@@ -42,9 +42,13 @@ def main():
         plans = {}
         for v in variants:
             k, var = v.split(":")
-            if k not in plans:
-                os.environ["SPMV_HW_KERNEL"] = k
+            if k not in plans:  # "sweep@512" = sweep kernel with 512-thread workgroups
+                kern, _, threads = k.partition("@")
+                os.environ["SPMV_HW_KERNEL"] = kern
+                if threads:
+                    os.environ["SPMV_SWEEP_THREADS"] = threads
                 plans[k] = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+                os.environ.pop("SPMV_SWEEP_THREADS", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val

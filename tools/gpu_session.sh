@@ -31,7 +31,7 @@ for s in $STEPS; do
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
     calib) run calib 300 tools/hbm_calib ;;
     ab) run ab 600 python tools/ab_variants.py ;;
-    absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants tiles:0,sweep:2,sweep:3,sweep:7,sweep:10,sweep:11,sweep:14,sweep:15 ;;
+    absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants sweep:3,sweep:15,sweep:17,sweep@512:3,sweep@512:17,sweep@256:3,sweep@256:17 --rounds 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
            tagc=$(echo $c | tr ' ' '_')
