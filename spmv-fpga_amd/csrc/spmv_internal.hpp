@@ -65,7 +65,7 @@ struct spmv_plan {
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
     uint32_t panel_rmax = 0;
-    int sweep_threads = kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)
+    int sweep_threads = spmvhw::kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)
     uint32_t *d_s_col = nullptr;
     uint16_t *d_s_row = nullptr;
     ValueType *d_s_val = nullptr;
