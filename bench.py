@@ -62,15 +62,25 @@ def parse():
 
 
 def setup_dist(args):
+    """One process per GPU. RCCL ('nccl') by default; SPMV_BENCH_BACKEND=gloo with fewer GPUs than
+    ranks is the single-GPU rehearsal of the multi-process path (ranks share device r % ndev)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    backend = os.environ.get("SPMV_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks but only {ndev} GPUs (use SPMV_BENCH_BACKEND=gloo to rehearse)")
+    dev_index = local % ndev
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, local
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, dev_index
 
 
 def barrier(world):
@@ -178,10 +188,7 @@ def main():
 
     nnz_local = st["nr_nzeros"]
     alg_local = st["algorithmic_bytes"]
-    t_nnz = torch.tensor([float(nnz_local), float(alg_local)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t_nnz)
-    nnz_all, alg_all = float(t_nnz[0]), float(t_nnz[1])
+    nnz_all, alg_all = spmv_dist.sum_over_ranks([float(nnz_local), float(alg_local)], dev)
     if world > 1 and args.scaling == "strong":
         # one matrix: x and the row_ptr sentinel count once, not once per rank
         alg_all -= (world - 1) * (st["nr_cols"] * np.dtype(dtype).itemsize + 4)
@@ -202,11 +209,9 @@ def main():
 
     exchange = None
     if world > 1:
-        counts = None
-        t_cnt = torch.zeros(world, dtype=torch.int64, device=dev)
-        t_cnt[rank] = st["nr_rows"]
-        dist.all_reduce(t_cnt)
-        counts = t_cnt.cpu().numpy()
+        cnt = [0.0] * world
+        cnt[rank] = float(st["nr_rows"])
+        counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
         row_begin = int(counts[:rank].sum())
         n_total = int(counts.sum())
         res = {}

@@ -21,6 +21,14 @@ import torch
 import torch.distributed as dist
 
 
+def _staged(t: torch.Tensor) -> torch.Tensor:
+    """gloo collectives run on host tensors (used by the CPU tests and the single-GPU
+    multi-process rehearsal); RCCL ('nccl') works on the device tensor directly."""
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        return t.cpu()
+    return t
+
+
 def row_slice(bounds, rank: int):
     return int(bounds[rank]), int(bounds[rank + 1])
 
@@ -29,6 +37,7 @@ def exchange_reduce(y_slice: torch.Tensor, row_begin: int, n_rows: int, dst: int
     """accum_results semantics: full-length partials summed into rank `dst`."""
     full = torch.zeros(n_rows, dtype=y_slice.dtype, device=y_slice.device)
     full[row_begin:row_begin + y_slice.numel()] = y_slice
+    full = _staged(full)
     dist.reduce(full, dst=dst, op=dist.ReduceOp.SUM)
     return full if dist.get_rank() == dst else None
 
@@ -40,8 +49,9 @@ def exchange_gather(y_slice: torch.Tensor, counts, dst: int = 0):
     maxc = int(max(counts))
     buf = torch.zeros(maxc, dtype=y_slice.dtype, device=y_slice.device)
     buf[:y_slice.numel()] = y_slice
+    buf = _staged(buf)
     if rank == dst:
-        parts = [torch.empty(maxc, dtype=y_slice.dtype, device=y_slice.device) for _ in range(world)]
+        parts = [torch.empty(maxc, dtype=buf.dtype, device=buf.device) for _ in range(world)]
         dist.gather(buf, gather_list=parts, dst=dst)
         return torch.cat([parts[r][:int(counts[r])] for r in range(world)])
     dist.gather(buf, dst=dst)
@@ -51,8 +61,17 @@ def exchange_gather(y_slice: torch.Tensor, counts, dst: int = 0):
 def max_over_ranks(value: float, device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     if dist.is_available() and dist.is_initialized():
+        t = _staged(t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(values, device):
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized():
+        t = _staged(t)
+        dist.all_reduce(t)
+    return [float(v) for v in t.tolist()]
 
 
 def slice_counts(bounds) -> np.ndarray:

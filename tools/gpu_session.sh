@@ -30,6 +30,8 @@ for s in $STEPS; do
     banded) run bench_banded 300 python bench.py --workload banded ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
     calib) run calib 300 tools/hbm_calib ;;
+    rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
+              SPMV_BENCH_BACKEND=gloo run rehearse_strong 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --scaling strong ;;
     ab) run ab 600 python tools/ab_variants.py ;;
     absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants sweep:3,sweep:15,sweep:17,sweep@512:3,sweep@512:17,sweep@256:3,sweep@256:17 --rounds 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
