@@ -233,7 +233,8 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_panel_ent})
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_panel_ent,
+                      (void *)d_s_cbase})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -243,7 +244,8 @@ spmv_plan::~spmv_plan()
 uint64_t spmv_plan::device_bytes() const
 {
     if (kernel == kKernelSweep)
-        return ent_pad * (sizeof(uint32_t) + sizeof(uint16_t) + sizeof(ValueType)) + (npanels + 1) * 8;
+        return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
+               (npanels + 1) * 8 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0);
     return nnz_pad * (sizeof(uint32_t) + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;
 }

@@ -34,6 +34,7 @@ constexpr int kTileNnz = kStep * kTileSteps;       // 512 entries per wave tile
 constexpr int kBlockThreads = 256;                 // 4 waves = 4 tiles per workgroup
 constexpr int kSweepThreads = 1024;                // default panel-sweep workgroup (16 waves, 1/CU)
 constexpr uint64_t kSweepLdsBytes = 160 * 1024;    // LDS of one CU holds the panel's y
+constexpr uint64_t kSweepChunk = 128;              // entries per packed chunk (one wave, 2 per lane)
 
 // plan kernels (spmv_plan_stats.kernel)
 constexpr int kKernelTiles = 0;  // flagged-tile wave kernel, x gathered through the caches
@@ -50,7 +51,7 @@ struct spmv_plan {
     bool has_empty = false;
     int kernel = 0;
     int variant = 0;           // tile-kernel variant bits (spmv_plan_set_variant)
-    int sweep_variant = 15;    // sweep-kernel variant bits (spmv_plan_set_variant, kernel 2)
+    int sweep_variant = 22;    // sweep-kernel variant bits (spmv_plan_set_variant, kernel 2)
 
     uint32_t *d_col = nullptr;
     ValueType *d_val = nullptr;
@@ -71,6 +72,8 @@ struct spmv_plan {
     ValueType *d_s_val = nullptr;
     uint32_t *d_panel_row = nullptr;
     uint32_t *d_panel_ent = nullptr;
+    uint32_t *d_s_cbase = nullptr;   // packed form: base column per 128-entry chunk
+    bool sweep_packed = false;
     double locality = -1.0;    // probe result used by the automatic kernel choice
 
     // timing (HIP events around the main kernel, on the launch stream)

@@ -15,7 +15,9 @@
 //   s_col u32[ent_pad]  column of each entry, panels contiguous, ascending column per panel
 //   s_row u16[ent_pad]  row inside the panel (padding entries use the scratch slot R_p)
 //   s_val V[ent_pad]    value
-//   panel_row u32[P+1]  row range of panel p; panel_ent u32[P+1] entry range (multiples of 4)
+//   panel_row u32[P+1]  row range of panel p; panel_ent u32[P+1] entry range (multiples of 128)
+// Packed form (default when every 128-entry chunk spans < 65536 columns, 12 B/entry):
+//   s_col u32 holds (row_in_panel << 16) | (column - s_cbase[chunk]); s_row is dropped.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -55,6 +57,10 @@ __device__ __forceinline__ void load4(const float *__restrict__ v, uint64_t e, f
 
 template <int E> struct EntryVec;
 template <> struct EntryVec<4> { typedef u32x4 C; typedef u16x4 R; };
+template <> struct EntryVec<1> {
+    typedef uint32_t C __attribute__((ext_vector_type(1)));
+    typedef uint16_t R __attribute__((ext_vector_type(1)));
+};
 template <> struct EntryVec<2> {
     typedef uint32_t C __attribute__((ext_vector_type(2)));
     typedef uint16_t R __attribute__((ext_vector_type(2)));
@@ -65,6 +71,8 @@ __device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o
 {
     if constexpr (E == 4) {
         load4<NT>(v, e, o);
+    } else if constexpr (E == 1) {
+        o[0] = lds_<NT>(v + e);
     } else if constexpr (sizeof(V) == 8) {
         const f64x2 a = lds_<NT>(reinterpret_cast<const f64x2 *>(v + e));
         o[0] = a.x; o[1] = a.y;
@@ -95,6 +103,9 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
         ylds[i] = V(0);
     __syncthreads();
     constexpr uint64_t kGroup = (uint64_t)E * T;  // entries per workgroup group
+    // branch-free body (see k_spmv_sweep_packed): out-of-range groups re-read the panel's last
+    // E entries and add into the scratch slot R
+    const uint64_t elast = e1 > e0 ? e1 - E : e0;
     for (uint64_t base = e0; base < e1; base += Q * kGroup) {
         CV c[Q];
         RV r[Q];
@@ -102,26 +113,24 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
         bool ok[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const uint64_t e = base + q * kGroup + (uint64_t)E * threadIdx.x;
+            uint64_t e = base + q * kGroup + (uint64_t)E * threadIdx.x;
             ok[q] = e < e1;
-            if (ok[q]) {
-                c[q] = lds_<NT>(reinterpret_cast<const CV *>(col + e));
-                r[q] = lds_<NT>(reinterpret_cast<const RV *>(row + e));
-                loadv<NT, E>(val, e, v[q]);
-            }
+            e = ok[q] ? e : elast;
+            c[q] = lds_<NT>(reinterpret_cast<const CV *>(col + e));
+            r[q] = lds_<NT>(reinterpret_cast<const RV *>(row + e));
+            loadv<NT, E>(val, e, v[q]);
         }
+        V xv[Q][E];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if (ok[q]) {
-                V xv[E];
+        for (int q = 0; q < Q; ++q)
 #pragma unroll
-                for (int j = 0; j < E; ++j)
-                    xv[j] = x[c[q][j]];
+            for (int j = 0; j < E; ++j)
+                xv[q][j] = x[c[q][j]];
 #pragma unroll
-                for (int j = 0; j < E; ++j)
-                    atomicAdd(&ylds[r[q][j]], v[q][j] * xv[j]);
-            }
-        }
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+            for (int j = 0; j < E; ++j)
+                atomicAdd(&ylds[ok[q] ? (uint32_t)r[q][j] : R], v[q][j] * xv[q][j]);
         if constexpr (SYNC)
             __syncthreads();
     }
@@ -210,6 +219,91 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_pipe(
         y[r0 + i] = ylds[i];
 }
 
+// Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
+// one u32 base column per 128-entry chunk (one wave instruction of 2-entry lanes). Panels are
+// padded to whole chunks, so the chunk of a wave is wave-uniform and its base is a scalar load.
+template <typename V, int T, int Q, bool NT>
+__global__ __launch_bounds__(T) void k_spmv_sweep_packed(
+    const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
+    const V *__restrict__ x, V *__restrict__ y)
+{
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    V *ylds = reinterpret_cast<V *>(smem);
+    const uint32_t p = blockIdx.x;
+    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
+    const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
+    for (uint32_t i = threadIdx.x; i <= R; i += T)
+        ylds[i] = V(0);
+    __syncthreads();
+    constexpr uint64_t kGroup = 2ull * T;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane2 = 2u * (threadIdx.x & 63);
+    // branch-free body: a group past the panel end re-reads the panel's last chunk (valid
+    // memory) and adds into the scratch slot R, so every load of the Q groups issues together
+    const uint64_t last_chunk = e1 > e0 ? e1 - 128 : e0;
+    for (uint64_t base = e0; base < e1; base += Q * kGroup) {
+        u32x2 w[Q];
+        uint32_t cb[Q];
+        V v[Q][2];
+        bool ok[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            uint64_t wbase = base + q * kGroup + 128ull * wave;  // this wave's chunk
+            ok[q] = wbase < e1;                                   // wave-uniform
+            wbase = ok[q] ? wbase : last_chunk;
+            const uint64_t e = wbase + lane2;
+            w[q] = lds_<NT>(reinterpret_cast<const u32x2 *>(rc + e));
+            cb[q] = cbase[wbase >> 7];
+            loadv<NT, 2>(val, e, v[q]);
+        }
+        V xv[Q][2];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            xv[q][0] = x[cb[q] + (w[q].x & 0xFFFFu)];
+            xv[q][1] = x[cb[q] + (w[q].y & 0xFFFFu)];
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            atomicAdd(&ylds[ok[q] ? (w[q].x >> 16) : R], v[q][0] * xv[q][0]);
+            atomicAdd(&ylds[ok[q] ? (w[q].y >> 16) : R], v[q][1] * xv[q][1]);
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < R; i += T)
+        y[r0 + i] = ylds[i];
+}
+
+// chunk c of 128 entries: base = min column; fails the plan's packing when the span >= 65536
+__global__ void k_sweep_chunk_base(const uint32_t *__restrict__ col, uint64_t nchunks, uint32_t *__restrict__ cbase,
+                                   uint32_t *__restrict__ bad)
+{
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks)
+        return;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (int k = 0; k < 128; ++k) {
+        const uint32_t v = col[c * 128 + k];
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    cbase[c] = lo;
+    if (hi - lo >= 65536u)
+        atomicOr(bad, 1u);
+}
+
+// in place: col[k] <- (row << 16) | (col - base)
+__global__ void k_sweep_pack_rc(uint32_t *__restrict__ col, const uint16_t *__restrict__ row,
+                                const uint32_t *__restrict__ cbase, uint64_t n)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    col[k] = ((uint32_t)row[k] << 16) | (col[k] - cbase[k >> 7]);
+}
+
 // sort key of every entry: (panel, column bucket); one thread per row
 __global__ void k_sweep_keys(const IndexType *__restrict__ rp, const IndexType *__restrict__ col,
                              const uint32_t *__restrict__ panel_row, uint32_t npanels, IndexType nrows,
@@ -274,8 +368,10 @@ __global__ void k_sweep_pad(uint32_t npanels, const uint32_t *__restrict__ panel
     if (p >= npanels)
         return;
     const uint32_t R = panel_row[p + 1] - panel_row[p];
-    for (uint64_t d = (uint64_t)poff[p] + (off[p + 1] - off[p]); d < poff[p + 1]; ++d) {
-        s_col[d] = 0;
+    const uint64_t first_pad = (uint64_t)poff[p] + (off[p + 1] - off[p]);
+    const uint32_t pad_col = first_pad > poff[p] ? s_col[first_pad - 1] : 0u;
+    for (uint64_t d = first_pad; d < poff[p + 1]; ++d) {
+        s_col[d] = pad_col;  // value 0: adds nothing; column kept near the panel's last one
         s_row[d] = (uint16_t)R;  // scratch slot, never written back
         s_val[d] = V(0);
     }
@@ -308,6 +404,42 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     hipLaunchKernelGGL((k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>), grid, block, lds, s, p.d_s_col, \
                        p.d_s_row, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y)
+    if (p.sweep_packed) {
+        if (p.sweep_variant == 15)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 2, true>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 20)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 4, true>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 8, true>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        return;
+    }
+    if (p.sweep_variant == 20) {
+        SWEEP(2, 4, true, true);
+        return;
+    }
+    if (p.sweep_variant == 21) {
+        SWEEP(4, 4, true, true);
+        return;
+    }
+    if (p.sweep_variant == 22) {
+        SWEEP(2, 8, true, true);
+        return;
+    }
+    if (p.sweep_variant == 23) {
+        SWEEP(1, 16, true, true);
+        return;
+    }
+    if (p.sweep_variant == 24) {
+        SWEEP(2, 8, true, false);
+        return;
+    }
+    if (p.sweep_variant == 25) {
+        SWEEP(1, 8, true, true);
+        return;
+    }
     if (p.sweep_variant & 16) {
         if (p.sweep_variant & 1)
             hipLaunchKernelGGL((k_spmv_sweep_pipe<ValueType, T, true>), grid, block, lds, s, p.d_s_col, p.d_s_row,
@@ -390,7 +522,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     for (uint32_t q = 0; q < P; ++q) {
         const uint64_t cnt = uint64_t(h_rp[prow[q + 1]]) - h_rp[prow[q]];
         off[q + 1] = (uint32_t)(off[q] + cnt);
-        poff[q + 1] = (uint32_t)(poff[q] + (cnt + 3) / 4 * 4);
+        poff[q + 1] = (uint32_t)(poff[q] + (cnt + kSweepChunk - 1) / kSweepChunk * kSweepChunk);
         rmax_used = std::max(rmax_used, prow[q + 1] - prow[q]);
     }
     p.npanels = P;
@@ -461,6 +593,35 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     hipLaunchKernelGGL((k_sweep_pad<ValueType>), dim3((P + 255) / 256), dim3(256), 0, s, P, p.d_panel_row, d_off,
                        d_poff, p.d_s_col, p.d_s_row, p.d_s_val);
     SW_TRY(hipGetLastError());
+    // 12-byte packed entries when every 128-entry chunk spans < 65536 columns
+    {
+        const uint64_t nchunks = p.ent_pad / kSweepChunk;
+        SW_TRY(hipMalloc((void **)&p.d_s_cbase, std::max<uint64_t>(nchunks, 1) * 4));
+        uint32_t *d_bad = d_off;  // reuse: d_off is no longer needed once the scatter ran
+        SW_TRY(hipStreamSynchronize(s));
+        SW_TRY(hipMemsetAsync(d_bad, 0, 4, s));
+        if (nchunks)
+            hipLaunchKernelGGL(k_sweep_chunk_base, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s,
+                               p.d_s_col, nchunks, p.d_s_cbase, d_bad);
+        SW_TRY(hipGetLastError());
+        uint32_t bad = 0;
+        SW_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
+        SW_TRY(hipStreamSynchronize(s));
+        const char *env = std::getenv("SPMV_SWEEP_PACKED");
+        const bool want = !(env && env[0] == '0');
+        if (!bad && want && p.ent_pad) {
+            hipLaunchKernelGGL(k_sweep_pack_rc, dim3((unsigned)((p.ent_pad + 255) / 256)), dim3(256), 0, s, p.d_s_col,
+                               p.d_s_row, p.d_s_cbase, p.ent_pad);
+            SW_TRY(hipGetLastError());
+            SW_TRY(hipStreamSynchronize(s));
+            SW_TRY(hipFree(p.d_s_row));
+            p.d_s_row = nullptr;
+            p.sweep_packed = true;
+        } else {
+            SW_TRY(hipFree(p.d_s_cbase));
+            p.d_s_cbase = nullptr;
+        }
+    }
     SW_TRY(hipStreamSynchronize(s));
 #undef SW_TRY
     cleanup();

@@ -42,13 +42,17 @@ def main():
         plans = {}
         for v in variants:
             k, var = v.split(":")
-            if k not in plans:  # "sweep@512" = sweep kernel with 512-thread workgroups
+            if k not in plans:  # "sweep@512" = 512-thread workgroups, "sweepU" = unpacked entries
                 kern, _, threads = k.partition("@")
+                if kern.endswith("U"):
+                    kern = kern[:-1]
+                    os.environ["SPMV_SWEEP_PACKED"] = "0"
                 os.environ["SPMV_HW_KERNEL"] = kern
                 if threads:
                     os.environ["SPMV_SWEEP_THREADS"] = threads
                 plans[k] = spmv_hw.Plan.from_device(lib, rp, col, val, n)
                 os.environ.pop("SPMV_SWEEP_THREADS", None)
+                os.environ.pop("SPMV_SWEEP_PACKED", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
@@ -75,6 +79,7 @@ def main():
                 res[v].append(ms)
         out = {"workload": wl, "dtype": a.dtype, "nnz": st["nr_nzeros"], "alg_bytes": st["algorithmic_bytes"],
                "plans": {k: {kk: p.stats()[kk] for kk in ("kernel", "nr_tiles", "device_bytes")} for k, p in plans.items()}}
+        # (device_bytes tells packed 12-B entries from unpacked 14-B ones)
         for v in variants:
             med = float(np.median(res[v]))
             out[v] = {"median_ms": round(med, 5), "min_ms": round(min(res[v]), 5),
