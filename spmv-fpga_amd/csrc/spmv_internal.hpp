@@ -74,6 +74,7 @@ struct spmv_plan {
     uint32_t *d_panel_ent = nullptr;
     uint32_t *d_s_cbase = nullptr;   // packed form: base column per 128-entry chunk
     bool sweep_packed = false;
+    bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)
     double locality = -1.0;    // probe result used by the automatic kernel choice
 
     // timing (HIP events around the main kernel, on the launch stream)

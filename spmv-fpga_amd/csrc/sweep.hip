@@ -17,7 +17,9 @@
 //   s_val V[ent_pad]    value
 //   panel_row u32[P+1]  row range of panel p; panel_ent u32[P+1] entry range (multiples of 128)
 // Packed form (default when every 128-entry chunk spans < 65536 columns, 12 B/entry):
-//   s_col u32 holds (row_in_panel << 16) | (column - s_cbase[chunk]); s_row is dropped.
+//   s_col u32 holds (row_in_panel << 16) | (column - s_cbase[chunk]); s_row is dropped; inside a
+//   chunk, word 2l+j holds entry 64j+l (k_sweep_lane_order) so one gather instruction covers 64
+//   consecutive columns-sorted entries.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -302,6 +304,22 @@ __global__ void k_sweep_pack_rc(uint32_t *__restrict__ col, const uint16_t *__re
     if (k >= n)
         return;
     col[k] = ((uint32_t)row[k] << 16) | (col[k] - cbase[k >> 7]);
+}
+
+// Lane-order permutation inside each 128-entry chunk: memory word 2l+j holds logical entry
+// 64j+l, so the j-th gather instruction of a wave covers 64 CONSECUTIVE entries (sorted by
+// column) and lanes whose columns share a 128-byte x line are served by one L2 request.
+template <typename V>
+__global__ void k_sweep_lane_order(const uint32_t *__restrict__ rc_in, const V *__restrict__ v_in, uint64_t n,
+                                   uint32_t *__restrict__ rc_out, V *__restrict__ v_out)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    const uint64_t c = k & ~(uint64_t)127, w = k & 127;
+    const uint64_t m = c + 2 * (w & 63) + (w >> 6);
+    rc_out[m] = rc_in[k];
+    v_out[m] = v_in[k];
 }
 
 // sort key of every entry: (panel, column bucket); one thread per row
@@ -617,6 +635,22 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             SW_TRY(hipFree(p.d_s_row));
             p.d_s_row = nullptr;
             p.sweep_packed = true;
+            const char *lo = std::getenv("SPMV_SWEEP_LANE_ORDER");
+            if (!(lo && lo[0] == '0')) {
+                uint32_t *rc2 = nullptr;
+                ValueType *v2 = nullptr;
+                SW_TRY(hipMalloc((void **)&rc2, p.ent_pad * 4));
+                SW_TRY(hipMalloc((void **)&v2, p.ent_pad * sizeof(ValueType)));
+                hipLaunchKernelGGL((k_sweep_lane_order<ValueType>), dim3((unsigned)((p.ent_pad + 255) / 256)), dim3(256),
+                                   0, s, p.d_s_col, p.d_s_val, p.ent_pad, rc2, v2);
+                SW_TRY(hipGetLastError());
+                SW_TRY(hipStreamSynchronize(s));
+                SW_TRY(hipFree(p.d_s_col));
+                SW_TRY(hipFree(p.d_s_val));
+                p.d_s_col = rc2;
+                p.d_s_val = v2;
+                p.sweep_lane_order = true;
+            }
         } else {
             SW_TRY(hipFree(p.d_s_cbase));
             p.d_s_cbase = nullptr;

@@ -47,12 +47,16 @@ def main():
                 if kern.endswith("U"):
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_PACKED"] = "0"
+                if kern.endswith("L"):  # packed, without the lane-order permutation
+                    kern = kern[:-1]
+                    os.environ["SPMV_SWEEP_LANE_ORDER"] = "0"
                 os.environ["SPMV_HW_KERNEL"] = kern
                 if threads:
                     os.environ["SPMV_SWEEP_THREADS"] = threads
                 plans[k] = spmv_hw.Plan.from_device(lib, rp, col, val, n)
                 os.environ.pop("SPMV_SWEEP_THREADS", None)
                 os.environ.pop("SPMV_SWEEP_PACKED", None)
+                os.environ.pop("SPMV_SWEEP_LANE_ORDER", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val

@@ -33,7 +33,7 @@ for s in $STEPS; do
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
               SPMV_BENCH_BACKEND=gloo run rehearse_strong 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --scaling strong ;;
     ab) run ab 600 python tools/ab_variants.py ;;
-    absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants sweepU:15,sweepU:20,sweepU:22,sweep:15,sweep:20,sweep:22 --rounds 5 ;;
+    absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants sweepL:20,sweep:15,sweep:20,sweep:22 --rounds 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
            tagc=$(echo $c | tr ' ' '_')
