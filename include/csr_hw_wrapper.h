@@ -98,8 +98,9 @@ int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
  * Sweep kernel: bit 0 = non-temporal entry loads, bit 1 = workgroup barrier per iteration,
  * bit 2 = two entry groups per thread per iteration, bit 3 = 2-entry groups instead of 4,
  * bit 4 = software-pipelined entry stream (bits 1-3 ignored); 20/21/22 = 4x2, 4x4, 8x2 entries
- * per thread per barrier (default 20 = 4x2; on the packed 12-byte entries of a plan built without
- * SPMV_SWEEP_PACKED=0, variants 15/20/22 select 2/4/8 groups). */
+ * per thread per barrier. On the packed 12-byte entries (plans built without SPMV_SWEEP_PACKED=0)
+ * 15/20/22 = 2/4/8 groups of 2 per barrier, 26-34 = barrier-free waves that may run at most
+ * 1-4 iterations ahead of the slowest wave of the workgroup (default 28 = 2 groups, lag 2). */
 int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */

@@ -370,7 +370,7 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
 
 int spmv_plan_set_variant(spmv_plan *p, int variant)
 {
-    if (!p || variant < 0 || variant > 31) {
+    if (!p || variant < 0 || variant > 63) {
         set_error("spmv_plan_set_variant: bad arguments");
         return 1;
     }

@@ -51,7 +51,7 @@ struct spmv_plan {
     bool has_empty = false;
     int kernel = 0;
     int variant = 0;           // tile-kernel variant bits (spmv_plan_set_variant)
-    int sweep_variant = 20;    // sweep-kernel variant bits (spmv_plan_set_variant, kernel 2)
+    int sweep_variant = 28;    // sweep-kernel variant bits (spmv_plan_set_variant, kernel 2)
 
     uint32_t *d_col = nullptr;
     ValueType *d_val = nullptr;

@@ -224,7 +224,10 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_pipe(
 // Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
 // one u32 base column per 128-entry chunk (one wave instruction of 2-entry lanes). Panels are
 // padded to whole chunks, so the chunk of a wave is wave-uniform and its base is a scalar load.
-template <typename V, int T, int Q, bool NT>
+// LAG = 0: one workgroup barrier per iteration. LAG = k > 0: no barrier; each wave publishes
+// its iteration count in LDS and only waits (s_sleep) while it is more than k iterations
+// ahead of the slowest wave, so the vector-memory pipe never drains at a common barrier.
+template <typename V, int T, int Q, bool NT, int LAG = 0>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
@@ -236,9 +239,13 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t p = blockIdx.x;
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
+    __shared__ uint32_t progress[T / 64];
     for (uint32_t i = threadIdx.x; i <= R; i += T)
         ylds[i] = V(0);
+    if (threadIdx.x < T / 64)
+        progress[threadIdx.x] = 0;
     __syncthreads();
+    uint32_t iter = 0;
     constexpr uint64_t kGroup = 2ull * T;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane2 = 2u * (threadIdx.x & 63);
@@ -271,7 +278,28 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
             atomicAdd(&ylds[ok[q] ? (w[q].x >> 16) : R], v[q][0] * xv[q][0]);
             atomicAdd(&ylds[ok[q] ? (w[q].y >> 16) : R], v[q][1] * xv[q][1]);
         }
-        __syncthreads();
+        if constexpr (LAG == 0) {
+            __syncthreads();
+        } else {
+            ++iter;
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_store(&progress[wave], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // wait while more than LAG iterations ahead of the slowest wave
+            for (;;) {
+                const uint32_t lane = threadIdx.x & 63;
+                uint32_t pr = lane < T / 64
+                                  ? __hip_atomic_load(&progress[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                  : 0xFFFFFFFFu;
+#pragma unroll
+                for (int d = 1; d < T / 64; d <<= 1) {
+                    const uint32_t o = __shfl_xor(pr, d, 64);
+                    pr = o < pr ? o : pr;
+                }
+                if (__builtin_amdgcn_readfirstlane(pr) + LAG >= iter)
+                    break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < R; i += T)
@@ -429,6 +457,33 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         else if (p.sweep_variant == 20)
             hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 4, true>), grid, block, lds, s, p.d_s_col,
                                p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 26)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 4, true, 1>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 27)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 4, true, 2>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 28)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 2, true, 2>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 30)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 2, true, 1>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 31)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 3, true, 2>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 32)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 1, true, 2>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 33)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 1, true, 4>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 34)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 2, true, 3>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
+        else if (p.sweep_variant == 29)
+            hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 2, true, 4>), grid, block, lds, s, p.d_s_col,
+                               p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
         else
             hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, 8, true>), grid, block, lds, s, p.d_s_col,
                                p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
@@ -500,7 +555,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     const IndexType n = p.nr_rows;
     const uint64_t nnz = p.nnz;
     // a workgroup of T threads gets T/1024 of one CU's LDS for its panel's y
-    const uint64_t lds_bytes = kSweepLdsBytes * p.sweep_threads / 1024;
+    const uint64_t lds_bytes = kSweepLdsBytes * p.sweep_threads / 1024 - 256;  // 256 B: static LDS
     const uint32_t rmax = (uint32_t)std::min<uint64_t>(lds_bytes / sizeof(ValueType) - 1, 65534);
     int cus = 256;
     {
