@@ -74,7 +74,7 @@ def main():
                     ref = y.clone()
                 else:
                     err = float(((ref - y).abs().max() / ref.abs().max().clamp_min(1e-300)).item())
-                    assert err < 1e-9, f"{v} changed the result ({err})"
+                    assert err < (1e-9 if a.dtype == "f64" else 1e-5), f"{v} changed the result ({err})"
                 plan.set_timing(True)
                 for _ in range(a.reps):
                     plan.run(x, y)

@@ -33,7 +33,7 @@ for s in $STEPS; do
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
               SPMV_BENCH_BACKEND=gloo run rehearse_strong 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --scaling strong ;;
     ab) run ab 600 python tools/ab_variants.py ;;
-    absweep) run absweep 600 python tools/ab_variants.py --workload powerlaw --variants sweep:20,sweep:28,sweep:30,sweep:31,sweep:32,sweep:33,sweep:34 --rounds 5 ;;
+    absweep) run absweep 600 python tools/ab_variants.py ${AB_ARGS:---workload powerlaw --variants sweep:20,sweep:28,sweep:30 --rounds 5} ;;
     counters) run counters 120 rocprofv3 -L ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
            tagc=$(echo $c | tr ' ' '_')
@@ -46,7 +46,7 @@ for s in $STEPS; do
     pmcx) i=0; for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM" \
                     "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_BUSY_avr" \
                     "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD"; do
-           i=$((i+1)); run pmcx_$i 240 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmcx_$i" -o run -- python tools/ab_variants.py --workload powerlaw --variants ${PMCX_VARIANTS:-sweep:20} --rounds 1 --reps 3
+           i=$((i+1)); run pmcx_$i 240 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmcx_$i" -o run -- python tools/ab_variants.py --workload powerlaw ${PMCX_ARGS:-} --variants ${PMCX_VARIANTS:-sweep:28} --rounds 1 --reps 3
          done ;;
     pmc_calib) for c in FETCH_SIZE WRITE_SIZE; do
            run pmccal_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmccal_$c" -o run -- tools/hbm_calib
