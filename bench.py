@@ -18,7 +18,8 @@ Multi-GPU (--gpus N, one process per GPU, torch.distributed over RCCL):
   The y exchange (RCCL reduce of partials = accum_results semantics, and RCCL gather of the
   disjoint slices) is timed separately and reported in "exchange".
 
-Extra JSON fields: roofline (dominant kernel k_spmv_tiles, HIP events on its launch stream),
+Extra JSON fields: roofline (dominant kernel of the plan: k_spmv_sweep_packed for the power-law
+matrix, k_spmv_tiles for the banded one; HIP events on its launch stream),
 cpu_baseline (the oracle's restatement of spmv_gold, 1 thread, on the host of the GPU box),
 parity (full-size componentwise-scaled error vs that oracle run).
 """
@@ -197,12 +198,21 @@ def main():
     eff_gbps = alg_all / (ms * 1e-3) / 1e9
     # roofline of the dominant kernel: algorithmic bytes of one launch / mean launch duration
     achieved = alg_local / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    # the dominant kernel of this plan; its PMC traffic is taken from profiles/traffic.json only
+    # when that summary was recorded for the same workload, size and kernel
+    if st["kernel"] == 2:
+        kname = "k_spmv_sweep_packed" if st["format"] & 2 else "k_spmv_sweep"
+    else:
+        kname = "k_spmv_tiles"
     traffic = None
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
             key = f"{desc['workload']}_{args.dtype}"
-            if key in tr and tr[key].get("nnz") == nnz_local:
+            if (key in tr and tr[key].get("nnz") == nnz_local
+                    and tr[key].get("kernel", "").split("<")[0] == kname
+                    and (kname != "k_spmv_tiles"  # template flag NARROW = format bit 0
+                         or tr[key]["kernel"].endswith("true>" if st["format"] & 1 else "false>"))):
                 traffic = tr[key]["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
@@ -257,12 +267,12 @@ def main():
             "roofline_pct": round(100.0 * eff_gbps / (HBM_PEAK_GBPS * world), 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "k_spmv_tiles", "kernel_ms": round(kernel_ms, 5),
+                         "kernel": kname, "kernel_ms": round(kernel_ms, 5),
                          "kernel_launches": launches, "alg_bytes_per_launch": alg_local},
             "cpu_baseline": cpu,
             "parity": parity,
             "exchange": exchange,
-            "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "nr_nonempty_rows")},
+            "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
             "setup_s": round(setup_s, 2),
         }
         print(json.dumps(out), flush=True)

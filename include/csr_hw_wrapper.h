@@ -77,9 +77,10 @@ typedef struct spmv_plan_stats {
     uint64_t device_bytes;       /* bytes of the hw representation resident in HBM */
     uint64_t algorithmic_bytes;  /* compulsory CSR bytes per SpMV, SURVEY.md §8(d) */
     int32_t device;              /* HIP device ordinal */
-    int32_t kernel;              /* 0 = flagged-tile gather, 1 = flagged-tile LDS x-window */
+    int32_t kernel;              /* 0 = flagged-tile gather, 2 = panel sweep */
     int32_t blocks;              /* column blocks of the representation */
-    int32_t lds_tiles_pct;       /* % of tiles served from an LDS x-window (kernel 1) */
+    int32_t format;              /* bit 0: 16-bit column offsets per tile (kernel 0); bit 1: packed
+                                    12/8-byte sweep entries; bit 2: lane-ordered chunks (kernel 2) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are

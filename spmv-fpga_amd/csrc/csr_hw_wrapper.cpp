@@ -123,11 +123,16 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
             die(std::string("create_csr_hw_matrix: ") + spmv_hw_last_error());
         spmv_plan_stats st;
         spmv_plan_get_stats(h->plan, &st);
-        const uint64_t val_bytes = h->plan->nnz_pad * sizeof(ValueType);
-        h->sub[0] = reinterpret_cast<BusDataType *>(h->plan->d_col);
+        const spmv_plan &pl = *h->plan;
+        const bool sweep = pl.kernel == kKernelSweep;
+        const uint64_t val_bytes = (sweep ? pl.ent_pad : pl.nnz_pad) * sizeof(ValueType);
+        // the index stream of the unit's representation (opaque device address)
+        h->sub[0] = sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)
+                    : pl.tile_narrow ? reinterpret_cast<BusDataType *>(pl.d_col16)
+                                     : reinterpret_cast<BusDataType *>(pl.d_col);
         h->nr_rows[0] = (IndexType)st.nr_nonempty_rows;
         h->nr_cols[0] = matrix->nr_cols;
-        h->nr_nzeros[0] = (IndexType)h->plan->nnz_pad;
+        h->nr_nzeros[0] = (IndexType)(sweep ? pl.ent_pad : pl.nnz_pad);
         h->nr_ci[0] = (IndexType)ceil16(st.device_bytes - val_bytes);
         h->nr_val[0] = (IndexType)ceil16(val_bytes);
         h->pub.submatrix = h->sub;

@@ -25,6 +25,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -76,10 +77,12 @@ __device__ __forceinline__ void emit(V sum, uint32_t r, bool to_head, V *__restr
         st<NTY>(y + (row_id ? row_id[r] : r), sum);
 }
 
-// VAR bit 0: non-temporal streamed loads (col, val, row-end bits); bit 1: non-temporal y stores
-template <typename V, int U, int VAR>
+// VAR bit 0: non-temporal streamed loads (col, val, row-end bits); bit 1: non-temporal y stores.
+// NARROW: columns are 16-bit offsets (col16) from the tile's base column (tile_cbase).
+template <typename V, int U, int VAR, bool NARROW>
 __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
-    const uint32_t *__restrict__ col, const V *__restrict__ val, const uint32_t *__restrict__ rowend,
+    const uint32_t *__restrict__ col, const uint16_t *__restrict__ col16, const uint32_t *__restrict__ tile_cbase,
+    const V *__restrict__ val, const uint32_t *__restrict__ rowend,
     const uint32_t *__restrict__ tile_info, const uint32_t *__restrict__ row_id,
     const V *__restrict__ x, V *__restrict__ y, V *__restrict__ head, V *__restrict__ tail,
     uint64_t nnz, uint64_t ntiles)
@@ -94,11 +97,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     uint32_t c[U][4];
     V v[U][4];
     uint32_t fl[U];
+    const uint32_t cbase = NARROW ? tile_cbase[t] : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t kb = k0 + (uint64_t)u * kStep;
-        const u32x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u32x4 *>(col + kb + 4 * lane));
-        c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
+        if constexpr (NARROW) {
+            const u16x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u16x4 *>(col16 + kb + 4 * lane));
+            c[u][0] = cbase + cc.x; c[u][1] = cbase + cc.y; c[u][2] = cbase + cc.z; c[u][3] = cbase + cc.w;
+        } else {
+            const u32x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u32x4 *>(col + kb + 4 * lane));
+            c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
+        }
         load_vals<(VAR & 1) != 0>(val, kb, lane, v[u]);
         fl[u] = (ld<(VAR & 1) != 0>(rowend + (kb >> 5) + (lane >> 3)) >> ((lane & 7) * 4)) & 0xFu;
     }
@@ -232,15 +241,25 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
         return hipSuccess;
     const uint64_t waves_per_block = kBlockThreads / kWave;
     const uint64_t blocks = (p.ntiles + waves_per_block - 1) / waves_per_block;
-#define SPMV_LAUNCH(VAR)                                                                          \
-    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps, VAR>), dim3((unsigned)blocks),         \
-                       dim3(kBlockThreads), 0, s, p.d_col, p.d_val, p.d_rowend, p.d_tile_info,      \
-                       p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.nnz, p.ntiles)
-    switch (p.variant & 3) {
-    case 0: SPMV_LAUNCH(0); break;
-    case 1: SPMV_LAUNCH(1); break;
-    case 2: SPMV_LAUNCH(2); break;
-    default: SPMV_LAUNCH(3); break;
+#define SPMV_LAUNCH(VAR, NARROW)                                                                  \
+    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps, VAR, NARROW>), dim3((unsigned)blocks), \
+                       dim3(kBlockThreads), 0, s, p.d_col, p.d_col16, p.d_tile_cbase, p.d_val,      \
+                       p.d_rowend, p.d_tile_info, p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.nnz, \
+                       p.ntiles)
+    if (p.tile_narrow) {
+        switch (p.variant & 3) {
+        case 0: SPMV_LAUNCH(0, true); break;
+        case 1: SPMV_LAUNCH(1, true); break;
+        case 2: SPMV_LAUNCH(2, true); break;
+        default: SPMV_LAUNCH(3, true); break;
+        }
+    } else {
+        switch (p.variant & 3) {
+        case 0: SPMV_LAUNCH(0, false); break;
+        case 1: SPMV_LAUNCH(1, false); break;
+        case 2: SPMV_LAUNCH(2, false); break;
+        default: SPMV_LAUNCH(3, false); break;
+        }
     }
 #undef SPMV_LAUNCH
     return hipGetLastError();
@@ -281,6 +300,68 @@ hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, u
     const uint64_t blocks = (nnz_pad + 255) / 256;
     hipLaunchKernelGGL((k_pack<ValueType>), dim3((unsigned)blocks), dim3(256), 0, s, d_col_src,
                        d_val_src, nnz, nnz_pad, ncols, d_col, d_val, d_bad);
+    return hipGetLastError();
+}
+
+// One wave per tile: min / max column of the tile's real entries (k < nnz).
+__global__ __launch_bounds__(256) void k_tile_span(const uint32_t *__restrict__ col, uint64_t nnz, uint64_t ntiles,
+                                                   uint32_t *__restrict__ cbase, uint32_t *__restrict__ bad)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= ntiles)
+        return;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+    for (int j = 0; j < kTileNnz / kWave; ++j) {
+        const uint64_t k = t * kTileNnz + (uint64_t)j * kWave + lane;
+        if (k < nnz) {
+            const uint32_t c = col[k];
+            lo = c < lo ? c : lo;
+            hi = c > hi ? c : hi;
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t l2 = __shfl_xor(lo, d, kWave), h2 = __shfl_xor(hi, d, kWave);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if (lane == 0) {
+        if (lo == 0xFFFFFFFFu)
+            lo = hi = 0u;  // a tile of padding only
+        cbase[t] = lo;
+        if (hi - lo >= 65536u)
+            atomicOr(bad, 1u);
+    }
+}
+
+__global__ void k_narrow(const uint32_t *__restrict__ col, uint64_t nnz, uint64_t nnz_pad,
+                         const uint32_t *__restrict__ cbase, uint16_t *__restrict__ col16)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz_pad)
+        return;
+    // padding entries gather x[cbase] (a valid column) with value 0 and no row end
+    col16[k] = k < nnz ? (uint16_t)(col[k] - cbase[k / kTileNnz]) : (uint16_t)0;
+}
+
+hipError_t launch_tile_span(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles, uint32_t *d_cbase,
+                            uint32_t *d_bad, hipStream_t s)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_tile_span, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, d_col, nnz, ntiles,
+                       d_cbase, d_bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_cbase,
+                         uint16_t *d_col16, hipStream_t s)
+{
+    if (nnz_pad == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_narrow, dim3((unsigned)((nnz_pad + 255) / 256)), dim3(256), 0, s, d_col, nnz, nnz_pad,
+                       d_cbase, d_col16);
     return hipGetLastError();
 }
 

@@ -14,6 +14,10 @@
 //                           replaces the reference's empty_rows_bitmap scatter
 //                           (csr_hw.cpp:1531-1565) with an index map.
 // Entries past nnz (padding to a whole tile) have col 0, value 0 and no row-end bit.
+// Narrow form (default when every tile's columns span < 65536, e.g. banded matrices): col is
+// replaced by col16 u16[nnz_pad] = col - tile_cbase[tile] and tile_cbase u32[ntiles], i.e. the
+// reference's block-relative 16-bit column field (csr_hw.cpp:288-292) with a per-tile block
+// base: 10 B/nnz fp64 and 6 B/nnz fp32 are streamed instead of 12 and 8.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -54,6 +58,9 @@ struct spmv_plan {
     int sweep_variant = 28;    // sweep-kernel variant bits (spmv_plan_set_variant, kernel 2)
 
     uint32_t *d_col = nullptr;
+    uint16_t *d_col16 = nullptr;     // narrow form (d_col freed)
+    uint32_t *d_tile_cbase = nullptr;
+    bool tile_narrow = false;
     ValueType *d_val = nullptr;
     uint32_t *d_rowend = nullptr;
     uint32_t *d_tile_info = nullptr;
@@ -99,6 +106,11 @@ hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, u
                        uint64_t nnz_pad, uint32_t ncols, uint32_t *d_col, ValueType *d_val,
                        uint32_t *d_bad, hipStream_t s);
 hipError_t launch_validate(const IndexType *d_col, uint64_t nnz, uint32_t ncols, uint32_t *d_bad, hipStream_t s);
+// tile column bases (min column of each tile's real entries); *d_bad |= 1 when a span >= 65536
+hipError_t launch_tile_span(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles, uint32_t *d_cbase,
+                            uint32_t *d_bad, hipStream_t s);
+hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_cbase,
+                         uint16_t *d_col16, hipStream_t s);
 
 // sweep.hip
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);

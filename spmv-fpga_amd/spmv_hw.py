@@ -77,7 +77,7 @@ class spmv_plan_stats(ctypes.Structure):
                 ("nr_tiles", ctypes.c_uint64), ("tile_nnz", ctypes.c_uint64),
                 ("device_bytes", ctypes.c_uint64), ("algorithmic_bytes", ctypes.c_uint64),
                 ("device", ctypes.c_int32), ("kernel", ctypes.c_int32), ("blocks", ctypes.c_int32),
-                ("lds_tiles_pct", ctypes.c_int32)]
+                ("format", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

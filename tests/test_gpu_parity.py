@@ -27,13 +27,17 @@ def torch():
     return t
 
 
-KERNELS = ["tiles", "sweep"]
+KERNELS = ["tiles", "tiles_wide", "sweep"]
+KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2}
 
 
 @pytest.fixture(params=KERNELS)
 def kernel(request, monkeypatch):
-    """Plans are built with SPMV_HW_KERNEL forced to each kernel in turn."""
-    monkeypatch.setenv("SPMV_HW_KERNEL", request.param)
+    """Plans are built with SPMV_HW_KERNEL forced to each kernel in turn; "tiles_wide" is the
+    tile kernel with 32-bit columns (SPMV_TILE_NARROW=0) instead of per-tile 16-bit offsets."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", request.param.split("_")[0])
+    if request.param == "tiles_wide":
+        monkeypatch.setenv("SPMV_TILE_NARROW", "0")
     return request.param
 
 
@@ -55,7 +59,9 @@ def run_device(torch, lib, row_ptr, col, val, x, nr_cols, poison=True, expect_ke
     stats = plan.stats()
     plan.destroy()
     if expect_kernel is not None:
-        assert stats["kernel"] == {"tiles": 0, "sweep": 2}[expect_kernel]
+        assert stats["kernel"] == KERNEL_ID[expect_kernel]
+        if expect_kernel == "tiles_wide":
+            assert not stats["format"] & 1
     return out, stats
 
 
@@ -192,7 +198,7 @@ def test_deterministic(torch, kernel, dtype):
     lib = spmv_hw.load(dtype)
     y1, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
     y2, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
-    if kernel == "tiles":
+    if kernel.startswith("tiles"):
         assert np.array_equal(y1.view(np.uint8), y2.view(np.uint8))
     else:
         assert oracle.scaled_error(row_ptr, col, val, x, y1, y2) <= TIGHT[np.dtype(dtype)]
@@ -251,6 +257,52 @@ def test_row_slices_match_whole_matrix(torch, kernel):
             y, _ = run_device(torch, lib, (rp - rp[0]).astype(np.uint32), col[rp[0]:rp[-1]], val[rp[0]:rp[-1]], x, n)
             parts.append(y)
         check(row_ptr, col, val, x, y_ref, np.concatenate(parts), np.float64)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_narrow_tiles_bitwise_equal_to_wide(torch, monkeypatch, dtype):
+    """16-bit per-tile column offsets change the bytes streamed, not the arithmetic: the narrow and
+    wide tile representations give bitwise identical y."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
+    lib = spmv_hw.load(dtype)
+    n = 300_000
+    rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
+    x = spmv_hw.gen_vector(lib, n, seed=3)
+    ys, fmts, nbytes = [], [], []
+    for narrow in ("1", "0"):
+        monkeypatch.setenv("SPMV_TILE_NARROW", narrow)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+        y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+        plan.run(x, y)
+        torch.cuda.synchronize()
+        st = plan.stats()
+        fmts.append(st["format"] & 1)
+        nbytes.append(st["device_bytes"])
+        ys.append(y.cpu().numpy())
+        plan.destroy()
+    assert fmts == [1, 0]
+    assert nbytes[1] - nbytes[0] >= 2 * 16 * n - 4 * (16 * n // 512 + 1)  # 2 B/nnz saved
+    assert np.array_equal(ys[0].view(np.uint8), ys[1].view(np.uint8))
+
+
+@pytest.mark.parametrize("span,narrow", [(65535, 1), (65536, 0)])
+def test_narrow_tiles_span_limit(torch, monkeypatch, span, narrow):
+    """A tile whose columns span >= 65536 keeps the whole plan on 32-bit columns."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
+    monkeypatch.delenv("SPMV_TILE_NARROW", raising=False)
+    lib = spmv_hw.load(np.float64)
+    m = 70_000
+    rng = np.random.default_rng(5)
+    n = 40
+    lens = np.full(n, 20)
+    lens[0] = 2
+    row_ptr, col, val, x = random_csr(rng, n, span - 8, lens, np.float64)
+    col += 8                      # every other column in [8, span)
+    col[0], col[1] = 7, 7 + span  # row 0 spans exactly `span` columns
+    x = rng.uniform(0, 1, size=m)
+    y, st = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel="tiles")
+    assert st["format"] & 1 == narrow
+    check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y, np.float64)
 
 
 def test_auto_kernel_choice(torch, monkeypatch):
