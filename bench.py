@@ -187,6 +187,18 @@ def main():
     ms = spmv_dist.max_over_ranks(ms_local, dev)
     kernel_ms_max = spmv_dist.max_over_ranks(kernel_ms, dev)
 
+    # iterative / persistent mode: the same K SpMVs replayed from one hipGraph
+    # (reported beside the headline, which stays one host launch per step)
+    plan.run_graph(x, y, args.steps, stream)  # capture + warm-up
+    torch.cuda.synchronize()
+    barrier(world)
+    tg0 = time.perf_counter()
+    plan.run_graph(x, y, args.steps, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    graph = {"iters": args.steps,
+             "ms_per_step": round(spmv_dist.max_over_ranks((time.perf_counter() - tg0) * 1e3 / args.steps, dev), 5)}
+
     nnz_local = st["nr_nzeros"]
     alg_local = st["algorithmic_bytes"]
     nnz_all, alg_all = spmv_dist.sum_over_ranks([float(nnz_local), float(alg_local)], dev)
@@ -272,6 +284,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "exchange": exchange,
+            "graph": graph,
             "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
             "setup_s": round(setup_s, 2),
         }

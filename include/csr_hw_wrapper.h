@@ -91,8 +91,15 @@ int spmv_plan_create_device(spmv_plan **plan, int device, IndexType nr_rows, Ind
 /* Build a plan from rows [row_begin, row_end) of a host CSR matrix. */
 int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *matrix,
                           IndexType row_begin, IndexType row_end);
-/* d_y[0:nr_rows) = A * d_x  (overwrite; empty rows get 0). Asynchronous on `stream`. */
+/* d_y[0:nr_rows) = A * d_x  (overwrite; empty rows get 0). Asynchronous on `stream`. Enqueues
+ * only kernels and memsets (when timing is off), so callers may capture it into their own
+ * hipGraph, e.g. an iterative solver's SpMV + update + RCCL all-gather step. */
 int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, void *stream);
+/* Iterative / persistent mode: `iters` consecutive SpMVs d_y = A * d_x, captured once into a
+ * hipGraph (re-captured when d_x, d_y or iters change) and replayed on `stream` per call, so
+ * back-to-back SpMVs pay no per-launch host cost. With timing on, one event pair brackets the
+ * whole graph (spmv_plan_get_timing then reports ms per graph). */
+int spmv_plan_run_graph(spmv_plan *plan, const ValueType *d_x, ValueType *d_y, int iters, void *stream);
 int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
 /* Kernel variant bits (performance experiments; every variant computes the same y).
  * Tile kernel: bit 0 = non-temporal streamed loads, bit 1 = non-temporal y stores (default 0).

@@ -266,6 +266,10 @@ spmv_plan::~spmv_plan()
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
         (void)hipEventDestroy(e);
+    if (gexec)
+        (void)hipGraphExecDestroy(gexec);
+    if (gstream)
+        (void)hipStreamDestroy(gstream);
 }
 
 uint64_t spmv_plan::device_bytes() const
@@ -334,21 +338,16 @@ int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *m, Ind
                                         m->values + base, false, s);
 }
 
-int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, void *stream)
+// Enqueues one SpMV (memset of y when rows can be empty, main kernel, tile fix-up) on s. Only
+// kernels and memsets are enqueued, so the sequence is capturable into a hipGraph.
+static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool timing)
 {
-    if (!cp) {
-        set_error("spmv_plan_run: null plan");
-        return 1;
-    }
-    spmv_plan *p = const_cast<spmv_plan *>(cp);
-    hipStream_t s = (hipStream_t)stream;
-    SPMV_TRY(hipSetDevice(p->device));
     if (p->nr_rows == 0)
         return 0;
     if (p->kernel != kKernelSweep && (p->has_empty || p->nnz == 0))
         SPMV_TRY(hipMemsetAsync(d_y, 0, size_t(p->nr_rows) * sizeof(ValueType), s));
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (p->timing) {
+    if (timing) {
         if (p->ev_used + 2 > p->ev.size()) {
             for (int i = 0; i < 2; ++i) {
                 hipEvent_t e;
@@ -363,14 +362,77 @@ int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, voi
     }
     if (p->kernel == kKernelSweep) {
         SPMV_TRY(launch_sweep(*p, d_x, d_y, s));
-        if (p->timing)
+        if (timing)
             SPMV_TRY(hipEventRecord(e1, s));
         return 0;
     }
     SPMV_TRY(launch_spmv(*p, d_x, d_y, s));
-    if (p->timing)
+    if (timing)
         SPMV_TRY(hipEventRecord(e1, s));
     SPMV_TRY(launch_fixup(*p, d_y, s));
+    return 0;
+}
+
+int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, void *stream)
+{
+    if (!cp) {
+        set_error("spmv_plan_run: null plan");
+        return 1;
+    }
+    spmv_plan *p = const_cast<spmv_plan *>(cp);
+    SPMV_TRY(hipSetDevice(p->device));
+    return run_impl(p, d_x, d_y, (hipStream_t)stream, p->timing);
+}
+
+int spmv_plan_run_graph(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int iters, void *stream)
+{
+    if (!p || iters < 1) {
+        set_error("spmv_plan_run_graph: null plan or iters < 1");
+        return 1;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    SPMV_TRY(hipSetDevice(p->device));
+    if (!p->gexec || p->gx != d_x || p->gy != d_y || p->giters != iters) {
+        if (p->gexec) {
+            SPMV_TRY(hipGraphExecDestroy(p->gexec));
+            p->gexec = nullptr;
+        }
+        if (!p->gstream)
+            SPMV_TRY(hipStreamCreateWithFlags(&p->gstream, hipStreamNonBlocking));
+        SPMV_TRY(hipStreamBeginCapture(p->gstream, hipStreamCaptureModeRelaxed));
+        int rc = 0;
+        for (int i = 0; i < iters && !rc; ++i)
+            rc = run_impl(p, d_x, d_y, p->gstream, false);
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(p->gstream, &g);
+        if (rc) {
+            if (g)
+                (void)hipGraphDestroy(g);
+            return rc;
+        }
+        SPMV_TRY(ec);
+        const hipError_t ei = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        SPMV_TRY(ei);
+        p->gx = d_x;
+        p->gy = d_y;
+        p->giters = iters;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (p->timing) {
+        for (int i = 0; p->ev_used + 2 > p->ev.size() && i < 2; ++i) {
+            hipEvent_t e;
+            SPMV_TRY(hipEventCreate(&e));
+            p->ev.push_back(e);
+        }
+        e0 = p->ev[p->ev_used];
+        e1 = p->ev[p->ev_used + 1];
+        p->ev_used += 2;
+        SPMV_TRY(hipEventRecord(e0, s));
+    }
+    SPMV_TRY(hipGraphLaunch(p->gexec, s));
+    if (p->timing)
+        SPMV_TRY(hipEventRecord(e1, s));
     return 0;
 }
 

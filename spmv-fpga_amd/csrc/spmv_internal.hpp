@@ -89,6 +89,13 @@ struct spmv_plan {
     std::vector<hipEvent_t> ev;   // pairs
     size_t ev_used = 0;
 
+    // spmv_plan_run_graph: `giters` SpMVs on (gx, gy) captured once, replayed per call
+    hipGraphExec_t gexec = nullptr;
+    hipStream_t gstream = nullptr;
+    const ValueType *gx = nullptr;
+    ValueType *gy = nullptr;
+    int giters = 0;
+
     uint64_t device_bytes() const;
     uint64_t algorithmic_bytes() const;
     ~spmv_plan();  // frees every device buffer and event (also on error paths)

@@ -89,7 +89,7 @@ EXPORTS = [
     "delete_csr_hw_matrix", "delete_csr_hw_y_vector", "delete_csr_hw_x_vector",
     "storage_overhead", "verification",
     "spmv_hw_units", "spmv_hw_value_bytes", "spmv_hw_last_error",
-    "spmv_plan_create_device", "spmv_plan_create_host", "spmv_plan_run", "spmv_plan_get_stats",
+    "spmv_plan_create_device", "spmv_plan_create_host", "spmv_plan_run", "spmv_plan_run_graph", "spmv_plan_get_stats",
     "spmv_plan_set_variant", "spmv_plan_set_timing", "spmv_plan_get_timing", "spmv_plan_destroy", "spmv_partition_rows",
     "spmv_gen_banded", "spmv_gen_powerlaw_row_ptr", "spmv_gen_fill", "spmv_gen_vector",
 ]
@@ -130,6 +130,7 @@ class Lib:
             "spmv_plan_create_host": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int,
                                                      ctypes.POINTER(self.csr_matrix), IndexType, IndexType]),
             "spmv_plan_run": (ctypes.c_int, [vp, vp, vp, vp]),
+            "spmv_plan_run_graph": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, vp]),
             "spmv_plan_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(spmv_plan_stats)]),
             "spmv_plan_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
             "spmv_plan_set_variant": (ctypes.c_int, [vp, ctypes.c_int]),
@@ -274,6 +275,11 @@ class Plan:
     def run(self, x, y, stream=None) -> None:
         self.lib._ok(self.lib.L.spmv_plan_run(self.h, x.data_ptr(), y.data_ptr(), _stream_ptr(stream)),
                      "spmv_plan_run")
+
+    def run_graph(self, x, y, iters: int = 1, stream=None) -> None:
+        """`iters` SpMVs y = A x replayed from a hipGraph captured on the first call."""
+        self.lib._ok(self.lib.L.spmv_plan_run_graph(self.h, x.data_ptr(), y.data_ptr(), int(iters),
+                                                    _stream_ptr(stream)), "spmv_plan_run_graph")
 
     def stats(self) -> dict:
         st = spmv_plan_stats()

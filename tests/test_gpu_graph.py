@@ -1,0 +1,109 @@
+"""Iterative / persistent mode: spmv_plan_run_graph replays a captured
+hipGraph of SpMVs, and spmv_plan_run is capturable into a caller's graph. Same parity bar as
+tests/test_gpu_parity.py (componentwise-scaled error vs the oracle); the tile kernel is also
+bitwise equal to its eager launch."""
+import numpy as np
+import pytest
+
+import oracle
+import spmv_hw
+from test_gpu_parity import TIGHT, kernel, torch  # noqa: F401  (fixtures)
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(lib, n=200_000, z=3_200_000):
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    return rp, col, val, x
+
+
+def _host(*ts):
+    return [t.cpu().numpy() for t in ts]
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_run_graph_matches_eager_and_oracle(torch, kernel, dtype):
+    lib = spmv_hw.load(dtype)
+    rp, col, val, x = _problem(lib)
+    n = x.numel()
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    y_eager = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y_eager)
+    y_g = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    for iters in (1, 4, 4):  # capture, re-capture (iters changed), replay
+        y_g.fill_(float("nan"))
+        plan.run_graph(x, y_g, iters)
+    torch.cuda.synchronize()
+    rp_h, c_h, v_h, x_h, ye, yg = _host(rp, col, val, x, y_eager, y_g)
+    rp_h, c_h = rp_h.view(np.uint32), c_h.view(np.uint32)
+    ref = oracle.spmv_gold(rp_h, c_h, v_h, x_h)
+    assert oracle.scaled_error(rp_h, c_h, v_h, x_h, ref, yg) <= TIGHT[np.dtype(dtype)]
+    if kernel.startswith("tiles"):
+        assert np.array_equal(ye.view(np.uint8), yg.view(np.uint8))
+    plan.destroy()
+
+
+def test_run_graph_recaptures_on_new_buffers(torch):
+    lib = spmv_hw.load(np.float64)
+    rp, col, val, x = _problem(lib, 50_000, 800_000)
+    n = x.numel()
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    y1 = torch.zeros(n, dtype=x.dtype, device="cuda")
+    y2 = torch.zeros(n, dtype=x.dtype, device="cuda")
+    x2 = 2 * x
+    plan.run_graph(x, y1, 2)
+    plan.run_graph(x2, y2, 2)  # different x and y: must not replay the first graph
+    torch.cuda.synchronize()
+    assert torch.allclose(2 * y1, y2, rtol=1e-12, atol=0)
+    plan.destroy()
+
+
+def test_run_graph_timing_counts_graph_launches(torch):
+    lib = spmv_hw.load(np.float64)
+    rp, col, val, x = _problem(lib, 50_000, 800_000)
+    n = x.numel()
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    y = torch.empty(n, dtype=x.dtype, device="cuda")
+    plan.run_graph(x, y, 8)
+    plan.set_timing(True)
+    for _ in range(3):
+        plan.run_graph(x, y, 8)
+    mean_ms, total_ms, launches = plan.timing()
+    assert launches == 3 and mean_ms > 0 and abs(total_ms - 3 * mean_ms) < 1e-9 + 1e-6 * total_ms
+    plan.destroy()
+
+
+def test_plan_run_is_capturable_into_a_torch_graph(torch, kernel):
+    """A caller's own graph: SpMV followed by an update of x, replayed (an iterative solver's
+    step; here x <- y / ||y||_inf, a power iteration on a square matrix)."""
+    lib = spmv_hw.load(np.float64)
+    rp, col, val, x = _problem(lib, 50_000, 800_000)
+    n = x.numel()
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    y = torch.empty(n, dtype=x.dtype, device="cuda")
+    x_ref = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up outside the capture
+        plan.run(x, y)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    x.copy_(x_ref)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        plan.run(x, y)
+        x.copy_(y / y.abs().max())
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    # the same three steps eagerly, checked against the oracle step by step
+    rp_h, c_h, v_h = _host(rp, col, val)
+    rp_h, c_h = rp_h.view(np.uint32), c_h.view(np.uint32)
+    xh = x_ref.cpu().numpy()
+    for _ in range(3):
+        yh = oracle.spmv_gold(rp_h, c_h, v_h, xh)
+        xh = yh / np.abs(yh).max()
+    err = np.abs(x.cpu().numpy() - xh).max()
+    assert err <= 1e-12, err
+    plan.destroy()

@@ -47,6 +47,9 @@ def main():
                 if kern.endswith("U"):
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_PACKED"] = "0"
+                if kern.endswith("W"):  # tile kernel with 32-bit columns (no narrow form)
+                    kern = kern[:-1]
+                    os.environ["SPMV_TILE_NARROW"] = "0"
                 if kern.endswith("L"):  # packed, without the lane-order permutation
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_LANE_ORDER"] = "0"
@@ -57,6 +60,7 @@ def main():
                 os.environ.pop("SPMV_SWEEP_THREADS", None)
                 os.environ.pop("SPMV_SWEEP_PACKED", None)
                 os.environ.pop("SPMV_SWEEP_LANE_ORDER", None)
+                os.environ.pop("SPMV_TILE_NARROW", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
