@@ -237,17 +237,22 @@ def main():
         row_begin = int(counts[:rank].sum())
         n_total = int(counts.sum())
         res = {}
-        for mode in ("gather", "reduce"):
+        for mode in ("gather", "reduce", "allgather"):
+            def exchange():
+                if mode == "gather":
+                    return spmv_dist.exchange_gather(y, counts)
+                if mode == "allgather":
+                    return spmv_dist.exchange_allgather(y, counts)
+                return spmv_dist.exchange_reduce(y, row_begin, n_total)
+
             for _ in range(2):  # warm the communicator
-                (spmv_dist.exchange_gather(y, counts) if mode == "gather"
-                 else spmv_dist.exchange_reduce(y, row_begin, n_total))
+                exchange()
             torch.cuda.synchronize()
             barrier(world)
             reps = 5
             te0 = time.perf_counter()
             for _ in range(reps):
-                (spmv_dist.exchange_gather(y, counts) if mode == "gather"
-                 else spmv_dist.exchange_reduce(y, row_begin, n_total))
+                exchange()
             torch.cuda.synchronize()
             barrier(world)
             res[f"{mode}_ms"] = round(spmv_dist.max_over_ranks((time.perf_counter() - te0) * 1e3 / reps, dev), 4)

@@ -8,11 +8,13 @@ loop csr_hw_wrapper.cpp:276-281). Here a CU is a GPU rank:
   * row_slice(): the nnz-balanced contiguous slice of rank r (spmv_partition_rows in the C-ABI,
     S1 rule without the FPGA alignment rules S2/S3);
   * x is generated/uploaded on every rank (replicated, no collective);
-  * the y merge is a real exchange step, done two ways over RCCL:
+  * the y merge is a real exchange step, done three ways over RCCL:
       - "reduce": every rank contributes a full-length partial y (zeros outside its slice) to
         an RCCL reduce(SUM) on rank 0 -- the literal accum_results '+=' mapping;
-      - "gather": ranks send only their disjoint slices to rank 0 (bandwidth-optimal).
-Both return the full y on rank 0 and None elsewhere.
+      - "gather": ranks send only their disjoint slices to rank 0 (bandwidth-optimal);
+      - "allgather" (iterative solvers): equal padded slices all-gathered so
+        every rank holds the full y as its next x (one RCCL all_gather_into_tensor).
+    reduce and gather return the full y on rank 0 and None elsewhere.
 """
 from __future__ import annotations
 
@@ -56,6 +58,28 @@ def exchange_gather(y_slice: torch.Tensor, counts, dst: int = 0):
         return torch.cat([parts[r][:int(counts[r])] for r in range(world)])
     dist.gather(buf, dst=dst)
     return None
+
+
+def exchange_allgather(y_slice: torch.Tensor, counts, out: torch.Tensor | None = None):
+    """Every rank receives the full y (e.g. as the next x of an iterative solver). Slices are
+    padded to the longest one so the collective is a single all_gather_into_tensor."""
+    world = dist.get_world_size()
+    maxc = int(max(counts))
+    buf = torch.zeros(maxc, dtype=y_slice.dtype, device=y_slice.device)
+    buf[:y_slice.numel()] = y_slice
+    buf = _staged(buf)
+    gathered = torch.empty(world * maxc, dtype=buf.dtype, device=buf.device)
+    dist.all_gather_into_tensor(gathered, buf)
+    parts = gathered.view(world, maxc)
+    n = int(np.sum(counts))
+    if out is None:
+        out = torch.empty(n, dtype=y_slice.dtype, device=y_slice.device)
+    off = 0
+    for r in range(world):
+        c = int(counts[r])
+        out[off:off + c].copy_(parts[r, :c])
+        off += c
+    return out
 
 
 def max_over_ranks(value: float, device) -> float:

@@ -1,6 +1,7 @@
 """World-size-2 (and 3) gloo runs of the multi-GPU layout on CPU: nnz-balanced row slices per
-rank, x replicated, and both RCCL exchange forms (reduce of full-length partials = the
-accum_results '+=' mapping; gather of disjoint slices) rebuilding the full y on rank 0.
+rank, x replicated, and the three RCCL exchange forms (reduce of full-length partials = the
+accum_results '+=' mapping; gather of disjoint slices to rank 0; all-gather of padded slices to
+every rank, the iterative-solver form) rebuilding the full y.
 The per-rank product here is the CPU oracle standing in for the GPU kernel (test only)."""
 import os
 import socket
@@ -51,20 +52,23 @@ def _worker(rank, world, port, mode, q):
         y_t = torch.from_numpy(y_local)
         if mode == "reduce":
             full = sdist.exchange_reduce(y_t, r0, n)
-        else:
+        elif mode == "gather":
             full = sdist.exchange_gather(y_t, sdist.slice_counts(bounds))
+        else:  # every rank receives the whole y (next x of an iterative solver)
+            full = sdist.exchange_allgather(y_t, sdist.slice_counts(bounds))
+            assert np.array_equal(full.numpy(), oracle.spmv_gold(row_ptr, col, val, x))
         m = sdist.max_over_ranks(float(rank), torch.device("cpu"))
         if rank == 0:
             y_ref = oracle.spmv_gold(row_ptr, col, val, x)
             q.put((np.array_equal(full.numpy(), y_ref), m, list(sdist.slice_counts(bounds))))
-        else:
+        elif mode != "allgather":
             assert full is None
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("mode", ["reduce", "gather"])
+@pytest.mark.parametrize("mode", ["reduce", "gather", "allgather"])
 def test_row_sliced_exchange_rebuilds_y(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
