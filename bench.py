@@ -199,6 +199,22 @@ def main():
     graph = {"iters": args.steps,
              "ms_per_step": round(spmv_dist.max_over_ranks((time.perf_counter() - tg0) * 1e3 / args.steps, dev), 5)}
 
+    # the Part-1 boundary (spmv_hw) hands over host buffers: PCIe cost of x in and y out,
+    # pinned host memory (reported only; never part of `value`)
+    host = {}
+    for name, t in (("x_h2d_ms", x), ("y_d2h_ms", y)):
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        reps = 3
+        torch.cuda.synchronize()
+        th0 = time.perf_counter()
+        dst = torch.empty_like(t) if name == "x_h2d_ms" else h  # x itself stays intact
+        src = h if name == "x_h2d_ms" else t
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        host[name] = round((time.perf_counter() - th0) * 1e3 / reps, 4)
+        del h, dst
+
     nnz_local = st["nr_nzeros"]
     alg_local = st["algorithmic_bytes"]
     nnz_all, alg_all = spmv_dist.sum_over_ranks([float(nnz_local), float(alg_local)], dev)
@@ -290,6 +306,7 @@ def main():
             "parity": parity,
             "exchange": exchange,
             "graph": graph,
+            "host_copy": host,
             "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
             "setup_s": round(setup_s, 2),
         }
