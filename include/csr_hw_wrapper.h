@@ -140,6 +140,21 @@ int spmv_gen_fill(IndexType n, IndexType m, uint64_t seed, uint64_t row_offset,
 int spmv_gen_vector(IndexType n, uint64_t seed, uint64_t offset, double lo, double hi,
                     ValueType *d_x, void *stream);
 
+/* ---------------- Part 3: fast matrix reader (host only) ----------------
+ * Parallel, memory-mapped replacements of the reference's text reader with the same call
+ * pattern and results (reader.cpp; threads: env SPMV_READ_THREADS, default min(16, cores)).
+ * Superset: MatrixMarket banner/comments (real|integer|pattern, general|symmetric|
+ * skew-symmetric, expanded), rows in any order, CRLF, index and count checks. */
+/* replaces read_csr_header (csr.cpp:10-46): 0 ok, 1 cannot open / EOF, 2 I/O, 3 parse error.
+ * nr_nzeros is the stored count (symmetric files expanded); blocks = 1. */
+int spmv_read_csr_header(csr_header *hdr, const char *filename);
+/* replaces read_csr_matrix (csr.cpp:87-136) on a matrix from create_csr_matrix(hdr)
+ * (csr.cpp:51-67): 0 ok, 1 parse error, 2 I/O error. Trailing empty rows are filled. */
+int spmv_read_csr_matrix(csr_matrix *matrix, const char *filename);
+/* header + malloc + read in one call; release the arrays with spmv_free_csr (or free()). */
+int spmv_read_csr(const char *filename, csr_matrix *out);
+void spmv_free_csr(csr_matrix *matrix);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,11 @@ def _structs(dtype):
     return csr_matrix, csr_vector, csr_hw_matrix, csr_hw_vector
 
 
+class csr_header(ctypes.Structure):  # csr.h:7-13
+    _fields_ = [("nr_rows", IndexType), ("nr_cols", IndexType), ("nr_nzeros", IndexType),
+                ("blocks", ctypes.c_int)]
+
+
 class spmv_plan_stats(ctypes.Structure):
     _fields_ = [("nr_rows", ctypes.c_uint64), ("nr_cols", ctypes.c_uint64),
                 ("nr_nzeros", ctypes.c_uint64), ("nr_nonempty_rows", ctypes.c_uint64),
@@ -92,6 +97,7 @@ EXPORTS = [
     "spmv_plan_create_device", "spmv_plan_create_host", "spmv_plan_run", "spmv_plan_run_graph", "spmv_plan_get_stats",
     "spmv_plan_set_variant", "spmv_plan_set_timing", "spmv_plan_get_timing", "spmv_plan_destroy", "spmv_partition_rows",
     "spmv_gen_banded", "spmv_gen_powerlaw_row_ptr", "spmv_gen_fill", "spmv_gen_vector",
+    "spmv_read_csr_header", "spmv_read_csr_matrix", "spmv_read_csr", "spmv_free_csr",
 ]
 
 
@@ -144,6 +150,10 @@ class Lib:
             "spmv_gen_fill": (ctypes.c_int, [IndexType, IndexType, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp, vp]),
             "spmv_gen_vector": (ctypes.c_int, [IndexType, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
                                                ctypes.c_double, vp, vp]),
+            "spmv_read_csr_header": (ctypes.c_int, [ctypes.POINTER(csr_header), ctypes.c_char_p]),
+            "spmv_read_csr_matrix": (ctypes.c_int, [ctypes.POINTER(self.csr_matrix), ctypes.c_char_p]),
+            "spmv_read_csr": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(self.csr_matrix)]),
+            "spmv_free_csr": (None, [ctypes.POINTER(self.csr_matrix)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -228,6 +238,28 @@ class Lib:
 
     def units(self) -> int:
         return int(self.L.spmv_hw_units())
+
+    # ---- Part 3: fast reader (host only) ----
+    def read_csr_header(self, path: str):
+        """spmv_read_csr_header: (rc, csr_header) with read_csr_header's codes (csr.cpp:10-46)."""
+        h = csr_header()
+        rc = self.L.spmv_read_csr_header(ctypes.byref(h), os.fsencode(path))
+        return rc, h
+
+    def read_csr(self, path: str):
+        """(row_ptr u32[n+1], col u32[nnz], val[nnz], nr_cols) copied out of spmv_read_csr."""
+        m = self.csr_matrix()
+        rc = self.L.spmv_read_csr(os.fsencode(path), ctypes.byref(m))
+        if rc != 0:
+            raise RuntimeError(f"spmv_read_csr({path}) = {rc}: {self.L.spmv_hw_last_error().decode()}")
+        try:
+            n, z = int(m.nr_rows), int(m.nr_nzeros)
+            rp = np.ctypeslib.as_array(m.row_ptr, (n + 1,)).copy()
+            col = np.ctypeslib.as_array(m.col_ind, (z,)).copy() if z else np.zeros(0, np.uint32)
+            val = np.ctypeslib.as_array(m.values, (z,)).copy() if z else np.zeros(0, self.dtype)
+            return rp.astype(np.uint32), col.astype(np.uint32), val, int(m.nr_cols)
+        finally:
+            self.L.spmv_free_csr(ctypes.byref(m))
 
     def partition_rows(self, row_ptr, units: int):
         row_ptr = np.ascontiguousarray(row_ptr, np.uint32)
