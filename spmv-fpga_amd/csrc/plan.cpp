@@ -239,9 +239,14 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             p->sweep_threads = v;
     }
     if (kernel == kKernelSweep) {
-        if (build_sweep(*p, h_row_ptr, d_col, d_val, s))
+        const int rc = build_sweep(*p, h_row_ptr, d_col, d_val, s);
+        if (rc == 2 && requested_kernel() != kKernelSweep) {
+            p->kernel = kernel = kKernelTiles;  // automatic choice: the tile layout has no such limit
+        } else if (rc) {
             return 1;
-    } else {
+        }
+    }
+    if (kernel != kKernelSweep) {
         if (build_tiles(*p, h_row_ptr, d_col, d_val, s))
             return 1;
     }

@@ -121,6 +121,7 @@ hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, 
 
 // sweep.hip
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);
+// 0 ok, 1 error, 2 the padded layout would overflow 32-bit entry offsets (caller may use tiles)
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s);
 int probe_locality(const IndexType *d_rp, const IndexType *d_col, IndexType n, hipStream_t s, double *frac);

@@ -706,11 +706,17 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     std::vector<uint32_t> off(P + 1), poff(P + 1);
     off[0] = poff[0] = 0;
     uint32_t rmax_used = 0;
+    uint64_t padded = 0;
     for (uint32_t q = 0; q < P; ++q) {
         const uint64_t cnt = uint64_t(h_rp[prow[q + 1]]) - h_rp[prow[q]];
+        padded += (cnt + kSweepChunk - 1) / kSweepChunk * kSweepChunk;
         off[q + 1] = (uint32_t)(off[q] + cnt);
-        poff[q + 1] = (uint32_t)(poff[q] + (cnt + kSweepChunk - 1) / kSweepChunk * kSweepChunk);
+        poff[q + 1] = (uint32_t)padded;
         rmax_used = std::max(rmax_used, prow[q + 1] - prow[q]);
+    }
+    if (padded > 0xFFFFFFFFull) {  // panel_ent is u32: the padded layout must fit (nnz near 2^32)
+        set_error("build_sweep: padded entry count exceeds 32 bits");
+        return 2;
     }
     p.npanels = P;
     p.panel_rmax = rmax_used;
