@@ -239,11 +239,23 @@ def main():
             key = f"{desc['workload']}_{args.dtype}"
             if (key in tr and tr[key].get("nnz") == nnz_local
                     and tr[key].get("kernel", "").split("<")[0] == kname
-                    and (kname != "k_spmv_tiles"  # template flag NARROW = format bit 0
-                         or tr[key]["kernel"].endswith("true>" if st["format"] & 1 else "false>"))):
+                    and (kname != "k_spmv_tiles"  # template arg CB: bytes per stored column
+                         or tr[key]["kernel"].endswith(
+                             ", %d>" % (1 if st["format"] & 8 else 2 if st["format"] & 1 else 4)))):
                 traffic = tr[key]["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
+
+    # the achievable HBM read rate measured on MI355X by tools/hbm_calib (dwordx4 stream read,
+    # SURVEY §8d "report both"); the roofline fraction stays against the 8 TB/s spec
+    stream_peak = None
+    try:
+        for line in open(os.path.join(ROOT, "profiles", "r01_hbm_calib.jsonl")):
+            rec = json.loads(line)
+            if rec.get("test") == "stream_read":
+                stream_peak = rec["GBps"]
+    except (OSError, ValueError):
+        stream_peak = None
 
     exchange = None
     if world > 1:
@@ -299,6 +311,8 @@ def main():
             "effective_GBps": round(eff_gbps, 2),
             "roofline_pct": round(100.0 * eff_gbps / (HBM_PEAK_GBPS * world), 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                         "peak_measured": stream_peak,
+                         "frac_of_measured": round(achieved / stream_peak, 4) if stream_peak else None,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel": kname, "kernel_ms": round(kernel_ms, 5),
                          "kernel_launches": launches, "alg_bytes_per_launch": alg_local},

@@ -128,7 +128,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         const uint64_t val_bytes = (sweep ? pl.ent_pad : pl.nnz_pad) * sizeof(ValueType);
         // the index stream of the unit's representation (opaque device address)
         h->sub[0] = sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)
-                    : pl.tile_narrow ? reinterpret_cast<BusDataType *>(pl.d_col16)
+                    : pl.tile_col_bytes < 4 ? reinterpret_cast<BusDataType *>(pl.d_colnar)
                                      : reinterpret_cast<BusDataType *>(pl.d_col);
         h->nr_rows[0] = (IndexType)st.nr_nonempty_rows;
         h->nr_cols[0] = matrix->nr_cols;

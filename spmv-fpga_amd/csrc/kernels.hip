@@ -78,10 +78,11 @@ __device__ __forceinline__ void emit(V sum, uint32_t r, bool to_head, V *__restr
 }
 
 // VAR bit 0: non-temporal streamed loads (col, val, row-end bits); bit 1: non-temporal y stores.
-// NARROW: columns are 16-bit offsets (col16) from the tile's base column (tile_cbase).
-template <typename V, int U, int VAR, bool NARROW>
+// CB = bytes per stored column: 4 = absolute (col), 2 / 1 = offsets (colnar) from the tile's
+// base column (tile_cbase).
+template <typename V, int U, int VAR, int CB>
 __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
-    const uint32_t *__restrict__ col, const uint16_t *__restrict__ col16, const uint32_t *__restrict__ tile_cbase,
+    const uint32_t *__restrict__ col, const void *__restrict__ colnar, const uint32_t *__restrict__ tile_cbase,
     const V *__restrict__ val, const uint32_t *__restrict__ rowend,
     const uint32_t *__restrict__ tile_info, const uint32_t *__restrict__ row_id,
     const V *__restrict__ x, V *__restrict__ y, V *__restrict__ head, V *__restrict__ tail,
@@ -97,13 +98,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     uint32_t c[U][4];
     V v[U][4];
     uint32_t fl[U];
-    const uint32_t cbase = NARROW ? tile_cbase[t] : 0u;
+    const uint32_t cbase = CB < 4 ? tile_cbase[t] : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t kb = k0 + (uint64_t)u * kStep;
-        if constexpr (NARROW) {
-            const u16x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u16x4 *>(col16 + kb + 4 * lane));
+        if constexpr (CB == 2) {
+            const u16x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u16x4 *>(colnar) + (kb / 4 + lane));
             c[u][0] = cbase + cc.x; c[u][1] = cbase + cc.y; c[u][2] = cbase + cc.z; c[u][3] = cbase + cc.w;
+        } else if constexpr (CB == 1) {
+            const uint32_t cc = ld<(VAR & 1) != 0>(reinterpret_cast<const uint32_t *>(colnar) + (kb / 4 + lane));
+            c[u][0] = cbase + (cc & 0xFFu); c[u][1] = cbase + ((cc >> 8) & 0xFFu);
+            c[u][2] = cbase + ((cc >> 16) & 0xFFu); c[u][3] = cbase + (cc >> 24);
         } else {
             const u32x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u32x4 *>(col + kb + 4 * lane));
             c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
@@ -241,26 +246,26 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
         return hipSuccess;
     const uint64_t waves_per_block = kBlockThreads / kWave;
     const uint64_t blocks = (p.ntiles + waves_per_block - 1) / waves_per_block;
-#define SPMV_LAUNCH(VAR, NARROW)                                                                  \
-    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps, VAR, NARROW>), dim3((unsigned)blocks), \
-                       dim3(kBlockThreads), 0, s, p.d_col, p.d_col16, p.d_tile_cbase, p.d_val,      \
+#define SPMV_LAUNCH(VAR, CB)                                                                      \
+    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps, VAR, CB>), dim3((unsigned)blocks),     \
+                       dim3(kBlockThreads), 0, s, p.d_col, p.d_colnar, p.d_tile_cbase, p.d_val,     \
                        p.d_rowend, p.d_tile_info, p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.nnz, \
                        p.ntiles)
-    if (p.tile_narrow) {
-        switch (p.variant & 3) {
-        case 0: SPMV_LAUNCH(0, true); break;
-        case 1: SPMV_LAUNCH(1, true); break;
-        case 2: SPMV_LAUNCH(2, true); break;
-        default: SPMV_LAUNCH(3, true); break;
-        }
-    } else {
-        switch (p.variant & 3) {
-        case 0: SPMV_LAUNCH(0, false); break;
-        case 1: SPMV_LAUNCH(1, false); break;
-        case 2: SPMV_LAUNCH(2, false); break;
-        default: SPMV_LAUNCH(3, false); break;
-        }
+#define SPMV_VARIANTS(CB)                    \
+    switch (p.variant & 3) {                 \
+    case 0: SPMV_LAUNCH(0, CB); break;       \
+    case 1: SPMV_LAUNCH(1, CB); break;       \
+    case 2: SPMV_LAUNCH(2, CB); break;       \
+    default: SPMV_LAUNCH(3, CB); break;      \
     }
+    if (p.tile_col_bytes == 1) {
+        SPMV_VARIANTS(1)
+    } else if (p.tile_col_bytes == 2) {
+        SPMV_VARIANTS(2)
+    } else {
+        SPMV_VARIANTS(4)
+    }
+#undef SPMV_VARIANTS
 #undef SPMV_LAUNCH
     return hipGetLastError();
 }
@@ -305,7 +310,7 @@ hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, u
 
 // One wave per tile: min / max column of the tile's real entries (k < nnz).
 __global__ __launch_bounds__(256) void k_tile_span(const uint32_t *__restrict__ col, uint64_t nnz, uint64_t ntiles,
-                                                   uint32_t *__restrict__ cbase, uint32_t *__restrict__ bad)
+                                                   uint32_t *__restrict__ cbase, uint32_t *__restrict__ maxspan)
 {
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -330,38 +335,41 @@ __global__ __launch_bounds__(256) void k_tile_span(const uint32_t *__restrict__ 
         if (lo == 0xFFFFFFFFu)
             lo = hi = 0u;  // a tile of padding only
         cbase[t] = lo;
-        if (hi - lo >= 65536u)
-            atomicOr(bad, 1u);
+        atomicMax(maxspan, hi - lo);
     }
 }
 
+template <typename T>
 __global__ void k_narrow(const uint32_t *__restrict__ col, uint64_t nnz, uint64_t nnz_pad,
-                         const uint32_t *__restrict__ cbase, uint16_t *__restrict__ col16)
+                         const uint32_t *__restrict__ cbase, T *__restrict__ out)
 {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nnz_pad)
         return;
     // padding entries gather x[cbase] (a valid column) with value 0 and no row end
-    col16[k] = k < nnz ? (uint16_t)(col[k] - cbase[k / kTileNnz]) : (uint16_t)0;
+    out[k] = k < nnz ? (T)(col[k] - cbase[k / kTileNnz]) : (T)0;
 }
 
 hipError_t launch_tile_span(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles, uint32_t *d_cbase,
-                            uint32_t *d_bad, hipStream_t s)
+                            uint32_t *d_maxspan, hipStream_t s)
 {
     if (ntiles == 0)
         return hipSuccess;
     hipLaunchKernelGGL(k_tile_span, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, d_col, nnz, ntiles,
-                       d_cbase, d_bad);
+                       d_cbase, d_maxspan);
     return hipGetLastError();
 }
 
 hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_cbase,
-                         uint16_t *d_col16, hipStream_t s)
+                         void *d_out, int bytes, hipStream_t s)
 {
     if (nnz_pad == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(k_narrow, dim3((unsigned)((nnz_pad + 255) / 256)), dim3(256), 0, s, d_col, nnz, nnz_pad,
-                       d_cbase, d_col16);
+    const dim3 grid((unsigned)((nnz_pad + 255) / 256)), block(256);
+    if (bytes == 1)
+        hipLaunchKernelGGL((k_narrow<uint8_t>), grid, block, 0, s, d_col, nnz, nnz_pad, d_cbase, (uint8_t *)d_out);
+    else
+        hipLaunchKernelGGL((k_narrow<uint16_t>), grid, block, 0, s, d_col, nnz, nnz_pad, d_cbase, (uint16_t *)d_out);
     return hipGetLastError();
 }
 

@@ -125,28 +125,32 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
         SPMV_TRY(hipMemcpyAsync(p.d_cross, cross.data(), cross.size() * 4, hipMemcpyHostToDevice, s));
     if (p.nnz_pad)
         SPMV_TRY(launch_pack(d_col_src, d_val_src, nnz, p.nnz_pad, p.nr_cols, p.d_col, p.d_val, nullptr, s));
-    // narrow form: 16-bit column offsets from a per-tile base when every tile allows it
+    // narrow form: 8- or 16-bit column offsets from a per-tile base when every tile allows it
+    // (env SPMV_TILE_NARROW: 0 = keep 32-bit columns, 16 = at most 16-bit, default narrowest)
     const char *nenv = std::getenv("SPMV_TILE_NARROW");
-    if (p.ntiles && !(nenv && nenv[0] == '0')) {
-        uint32_t *d_bad = nullptr;
+    const int narrow_min = !nenv || !*nenv ? 1 : std::atoi(nenv) == 16 ? 2 : std::atoi(nenv) == 0 ? 4 : 1;
+    if (p.ntiles && narrow_min < 4) {
+        uint32_t *d_span = nullptr;
         SPMV_TRY(alloc((void **)&p.d_tile_cbase, p.ntiles * sizeof(uint32_t)));
-        SPMV_TRY(alloc((void **)&d_bad, sizeof(uint32_t)));
-        SPMV_TRY(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s));
-        uint32_t bad = 1;
-        hipError_t e = launch_tile_span(p.d_col, nnz, p.ntiles, p.d_tile_cbase, d_bad, s);
+        SPMV_TRY(alloc((void **)&d_span, sizeof(uint32_t)));
+        uint32_t span = 0xFFFFFFFFu;
+        hipError_t e = hipMemsetAsync(d_span, 0, sizeof(uint32_t), s);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+            e = launch_tile_span(p.d_col, nnz, p.ntiles, p.d_tile_cbase, d_span, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(&span, d_span, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess)
             e = hipStreamSynchronize(s);
-        (void)hipFree(d_bad);
+        (void)hipFree(d_span);
         SPMV_TRY(e);
-        if (!bad) {
-            SPMV_TRY(alloc((void **)&p.d_col16, p.nnz_pad * sizeof(uint16_t)));
-            SPMV_TRY(launch_narrow(p.d_col, nnz, p.nnz_pad, p.d_tile_cbase, p.d_col16, s));
+        const int cb = span < 256u && narrow_min <= 1 ? 1 : span < 65536u ? 2 : 4;
+        if (cb < 4) {
+            SPMV_TRY(alloc(&p.d_colnar, p.nnz_pad * cb));
+            SPMV_TRY(launch_narrow(p.d_col, nnz, p.nnz_pad, p.d_tile_cbase, p.d_colnar, cb, s));
             SPMV_TRY(hipStreamSynchronize(s));
             SPMV_TRY(hipFree(p.d_col));
             p.d_col = nullptr;
-            p.tile_narrow = true;
+            p.tile_col_bytes = cb;
         } else {
             SPMV_TRY(hipFree(p.d_tile_cbase));
             p.d_tile_cbase = nullptr;
@@ -266,7 +270,7 @@ spmv_plan::~spmv_plan()
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
                       (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_panel_ent,
-                      (void *)d_s_cbase, (void *)d_col16, (void *)d_tile_cbase})
+                      (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -282,8 +286,8 @@ uint64_t spmv_plan::device_bytes() const
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 8 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0);
-    return nnz_pad * ((tile_narrow ? sizeof(uint16_t) : sizeof(uint32_t)) + sizeof(ValueType)) + nnz_pad / 8 +
-           (ntiles + 1) * 4 + (tile_narrow ? ntiles * 4 : 0) +
+    return nnz_pad * (tile_col_bytes + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
+           (tile_col_bytes < 4 ? ntiles * 4 : 0) +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;
 }
 
@@ -459,7 +463,8 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->device = p->device;
     st->kernel = p->kernel;
     st->blocks = 1;
-    st->format = (p->tile_narrow ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0);
+    st->format = (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) |
+                 (p->tile_col_bytes == 1 ? 8 : 0);
     return 0;
 }
 

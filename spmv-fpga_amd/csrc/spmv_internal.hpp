@@ -15,9 +15,10 @@
 //                           (csr_hw.cpp:1531-1565) with an index map.
 // Entries past nnz (padding to a whole tile) have col 0, value 0 and no row-end bit.
 // Narrow form (default when every tile's columns span < 65536, e.g. banded matrices): col is
-// replaced by col16 u16[nnz_pad] = col - tile_cbase[tile] and tile_cbase u32[ntiles], i.e. the
-// reference's block-relative 16-bit column field (csr_hw.cpp:288-292) with a per-tile block
-// base: 10 B/nnz fp64 and 6 B/nnz fp32 are streamed instead of 12 and 8.
+// replaced by colnar u16[nnz_pad] (u8 when every span < 256) = col - tile_cbase[tile] and
+// tile_cbase u32[ntiles], i.e. the reference's block-relative 16-bit column field
+// (csr_hw.cpp:288-292) with a per-tile block base: 10 (9) B/nnz fp64 and 6 (5) B/nnz fp32 are
+// streamed instead of 12 and 8.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -58,9 +59,9 @@ struct spmv_plan {
     int sweep_variant = 28;    // sweep-kernel variant bits (spmv_plan_set_variant, kernel 2)
 
     uint32_t *d_col = nullptr;
-    uint16_t *d_col16 = nullptr;     // narrow form (d_col freed)
+    void *d_colnar = nullptr;        // narrow form: u16 or u8 offsets from tile_cbase (d_col freed)
     uint32_t *d_tile_cbase = nullptr;
-    bool tile_narrow = false;
+    int tile_col_bytes = 4;          // 4 (d_col), 2 or 1 (d_colnar)
     ValueType *d_val = nullptr;
     uint32_t *d_rowend = nullptr;
     uint32_t *d_tile_info = nullptr;
@@ -113,11 +114,13 @@ hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, u
                        uint64_t nnz_pad, uint32_t ncols, uint32_t *d_col, ValueType *d_val,
                        uint32_t *d_bad, hipStream_t s);
 hipError_t launch_validate(const IndexType *d_col, uint64_t nnz, uint32_t ncols, uint32_t *d_bad, hipStream_t s);
-// tile column bases (min column of each tile's real entries); *d_bad |= 1 when a span >= 65536
+// tile column bases (min column of each tile's real entries); *d_maxspan = max over tiles of
+// (max column - min column)
 hipError_t launch_tile_span(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles, uint32_t *d_cbase,
-                            uint32_t *d_bad, hipStream_t s);
+                            uint32_t *d_maxspan, hipStream_t s);
+// col - cbase[tile] as `bytes`-wide offsets (2 or 1)
 hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_cbase,
-                         uint16_t *d_col16, hipStream_t s);
+                         void *d_out, int bytes, hipStream_t s);
 
 // sweep.hip
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);

@@ -261,33 +261,37 @@ def test_row_slices_match_whole_matrix(torch, kernel):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_narrow_tiles_bitwise_equal_to_wide(torch, monkeypatch, dtype):
-    """16-bit per-tile column offsets change the bytes streamed, not the arithmetic: the narrow and
-    wide tile representations give bitwise identical y."""
+    """8- and 16-bit per-tile column offsets change the bytes streamed, not the arithmetic: all
+    three tile representations give bitwise identical y."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
     lib = spmv_hw.load(dtype)
     n = 300_000
     rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
     x = spmv_hw.gen_vector(lib, n, seed=3)
     ys, fmts, nbytes = [], [], []
-    for narrow in ("1", "0"):
+    for narrow in ("", "16", "0"):
         monkeypatch.setenv("SPMV_TILE_NARROW", narrow)
         plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
         y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
         plan.run(x, y)
         torch.cuda.synchronize()
         st = plan.stats()
-        fmts.append(st["format"] & 1)
+        fmts.append(st["format"] & 9)
         nbytes.append(st["device_bytes"])
         ys.append(y.cpu().numpy())
         plan.destroy()
-    assert fmts == [1, 0]
-    assert nbytes[1] - nbytes[0] >= 2 * 16 * n - 4 * (16 * n // 512 + 1)  # 2 B/nnz saved
-    assert np.array_equal(ys[0].view(np.uint8), ys[1].view(np.uint8))
+    assert fmts == [9, 1, 0]  # banded tiles span < 256 columns: 8-bit by default
+    z = 16 * n
+    assert nbytes[2] - nbytes[1] >= 2 * z - 4 * (z // 512 + 1)  # 2 B/nnz saved
+    assert nbytes[1] - nbytes[0] == z + (-z) % 512                  # 1 more B/nnz
+    for y in ys[1:]:
+        assert np.array_equal(ys[0].view(np.uint8), y.view(np.uint8))
 
 
-@pytest.mark.parametrize("span,narrow", [(65535, 1), (65536, 0)])
+@pytest.mark.parametrize("span,narrow", [(255, 9), (256, 1), (65535, 1), (65536, 0)])
 def test_narrow_tiles_span_limit(torch, monkeypatch, span, narrow):
-    """A tile whose columns span >= 65536 keeps the whole plan on 32-bit columns."""
+    """The widest tile decides the plan's column width: span < 256 -> 8-bit offsets,
+    < 65536 -> 16-bit, else 32-bit columns."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
     monkeypatch.delenv("SPMV_TILE_NARROW", raising=False)
     lib = spmv_hw.load(np.float64)
@@ -301,7 +305,7 @@ def test_narrow_tiles_span_limit(torch, monkeypatch, span, narrow):
     col[0], col[1] = 7, 7 + span  # row 0 spans exactly `span` columns
     x = rng.uniform(0, 1, size=m)
     y, st = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel="tiles")
-    assert st["format"] & 1 == narrow
+    assert st["format"] & 9 == narrow
     check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y, np.float64)
 
 

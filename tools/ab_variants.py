@@ -47,6 +47,9 @@ def main():
                 if kern.endswith("U"):
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_PACKED"] = "0"
+                if kern.endswith("H"):  # tile kernel with at most 16-bit column offsets
+                    kern = kern[:-1]
+                    os.environ["SPMV_TILE_NARROW"] = "16"
                 if kern.endswith("W"):  # tile kernel with 32-bit columns (no narrow form)
                     kern = kern[:-1]
                     os.environ["SPMV_TILE_NARROW"] = "0"
