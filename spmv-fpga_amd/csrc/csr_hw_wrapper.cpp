@@ -13,6 +13,7 @@
 #include <iomanip>
 #include <iostream>
 #include <mutex>
+#include <thread>
 
 #include "spmv_internal.hpp"
 
@@ -56,6 +57,10 @@ struct hw_matrix_impl {
     spmv_plan *plan = nullptr;
     int unit = 0, device = 0;
     IndexType row_begin = 0, row_end = 0;
+    // spmv_hw scratch, kept across calls: the unit's y slice on its GPU and a pinned host
+    // staging copy (the reference allocates its y per call, csr_hw_wrapper.cpp:198,287)
+    ValueType *d_y = nullptr;
+    ValueType *h_stage = nullptr;
     BusDataType *sub[1] = {nullptr};
     IndexType nr_rows[1] = {0}, nr_cols[1] = {0}, nr_nzeros[1] = {0}, nr_ci[1] = {0}, nr_val[1] = {0};
 };
@@ -234,15 +239,28 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         die("spmv_hw: null argument");
     const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
     hw_vector_impl *x = impl(hw_x);
-    csr_hw_vector **hw_y = nullptr;
-    create_csr_hw_y_vector(hw_matrix, &hw_y);
+    for (int u = 0; u < units; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        const IndexType rows = m->row_end - m->row_begin;
+        if (m->row_end > y_fpga->nr_values)
+            die("spmv_hw: y_fpga is shorter than the matrix has rows");
+        if ((size_t)m->device >= x->per_device.size())
+            die("spmv_hw: x vector was not uploaded to device " + std::to_string(m->device));
+        if (rows && !m->d_y) {
+            check(hipSetDevice(m->device), "hipSetDevice");
+            check(hipMalloc((void **)&m->d_y, size_t(rows) * sizeof(ValueType)), "hipMalloc(y)");
+            check(hipHostMalloc((void **)&m->h_stage, size_t(rows) * sizeof(ValueType), hipHostMallocDefault),
+                  "hipHostMalloc(y stage)");
+        }
+    }
 
+    // kernels of every unit (one stream per unit; units on different GPUs run concurrently)
     const double hw_s = timestamp_us();
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
-        if ((size_t)m->device >= x->per_device.size())
-            die("spmv_hw: x vector was not uploaded to device " + std::to_string(m->device));
-        if (spmv_plan_run(m->plan, x->per_device[m->device], impl(hw_y[u])->per_device[0], unit_stream(u)))
+        if (m->row_end == m->row_begin)
+            continue;
+        if (spmv_plan_run(m->plan, x->per_device[m->device], m->d_y, unit_stream(u)))
             die(std::string("spmv_hw: ") + spmv_hw_last_error());
     }
     for (int u = 0; u < units; ++u) {
@@ -252,29 +270,49 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
     const double hw_exec = (timestamp_us() - hw_s) / 1000.0;
     std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
 
+    // accum_results: every unit's slice comes back over its own PCIe link into pinned memory
+    // (all copies in flight together), then is added into y_fpga by a few host threads
     const double ra_s = timestamp_us();
-    std::vector<ValueType> stage;
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
         const IndexType rows = m->row_end - m->row_begin;
         if (!rows)
             continue;
-        if (m->row_end > y_fpga->nr_values)
-            die("spmv_hw: y_fpga is shorter than the matrix has rows");
-        stage.resize(rows);
         check(hipSetDevice(m->device), "hipSetDevice");
-        check(hipMemcpy(stage.data(), impl(hw_y[u])->per_device[0], size_t(rows) * sizeof(ValueType),
-                        hipMemcpyDeviceToHost),
-              "hipMemcpy(y)");
+        check(hipMemcpyAsync(m->h_stage, m->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost,
+                             unit_stream(u)),
+              "hipMemcpyAsync(y)");
+    }
+    const unsigned hc = std::thread::hardware_concurrency();
+    for (int u = 0; u < units; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        const IndexType rows = m->row_end - m->row_begin;
+        if (!rows)
+            continue;
+        check(hipSetDevice(m->device), "hipSetDevice");
+        check(hipStreamSynchronize(unit_stream(u)), "y copy");
         ValueType *dst = y_fpga->values + m->row_begin;
-        for (IndexType i = 0; i < rows; ++i)
-            dst[i] += stage[i];
+        const ValueType *src = m->h_stage;
+        const int T = rows < (1u << 20) ? 1 : (int)std::min(8u, hc ? hc : 1u);
+        auto add = [&](int t) {
+            const uint64_t b = uint64_t(rows) * t / T, e = uint64_t(rows) * (t + 1) / T;
+            for (uint64_t i = b; i < e; ++i)
+                dst[i] += src[i];
+        };
+        if (T == 1) {
+            add(0);
+        } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < T; ++t)
+                th.emplace_back(add, t);
+            for (auto &t : th)
+                t.join();
+        }
     }
     const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
     std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
     std::printf("Total time  : %.6f ms elapsed\n", hw_exec + ra_exec);
     std::fflush(stdout);
-    delete_csr_hw_y_vector(hw_y);
 }
 
 // csr_hw_wrapper.cpp:291-296
@@ -288,6 +326,13 @@ void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix)
             continue;
         hw_matrix_impl *m = impl(hw_matrix[u]);
         spmv_plan_destroy(m->plan);
+        if (m->d_y || m->h_stage) {
+            (void)hipSetDevice(m->device);
+            if (m->d_y)
+                (void)hipFree(m->d_y);
+            if (m->h_stage)
+                (void)hipHostFree(m->h_stage);
+        }
         delete m;
     }
     std::free(hw_matrix);
