@@ -223,10 +223,12 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
 
     int kernel = requested_kernel();
     if (kernel < 0) {
-        // automatic choice: the sweep pays when x is far larger than the L2s and the columns of a
-        // row are scattered (the first two columns of sampled rows lie >= 64 apart)
+        // automatic choice: the sweep pays once x outgrows ~half an XCD's L2 and the columns of a
+        // row are scattered (the first two columns of sampled rows lie >= 64 apart). Measured on
+        // power-law matrices with 16 nnz/row (profiles/r01_ab_variants.jsonl): tie at x = 1.6 MB,
+        // sweep 1.2x faster at 2.4 MB, 2.3x at 8 MB, 3.4x at 16 MB, 3.9x at 80 MB.
         kernel = kKernelTiles;
-        if (nnz && uint64_t(nr_cols) * sizeof(ValueType) > (32ull << 20) && nnz >= 16ull * kSweepThreads) {
+        if (nnz && uint64_t(nr_cols) * sizeof(ValueType) >= (2ull << 20) && nnz >= 16ull * kSweepThreads) {
             SPMV_TRY(hipMalloc(&trp.p, (size_t(nr_rows) + 1) * sizeof(IndexType)));
             SPMV_TRY(hipMemcpyAsync(trp.p, h_row_ptr, (size_t(nr_rows) + 1) * sizeof(IndexType),
                                     hipMemcpyHostToDevice, s));
