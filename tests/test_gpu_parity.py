@@ -320,3 +320,8 @@ def test_auto_kernel_choice(torch, monkeypatch):
     del rp, col, val
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 16 * n)
     assert spmv_hw.Plan.from_device(lib, rp, col, val, n).stats()["kernel"] == 2
+    del rp, col, val
+    # around the measured crossover: x of 2.4 MB -> sweep, x of 0.8 MB -> tiles
+    for n, want in ((300_000, 2), (100_000, 0)):
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 16 * n)
+        assert spmv_hw.Plan.from_device(lib, rp, col, val, n).stats()["kernel"] == want, n
