@@ -102,14 +102,13 @@ int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, v
  * whole graph (spmv_plan_get_timing then reports ms per graph). */
 int spmv_plan_run_graph(spmv_plan *plan, const ValueType *d_x, ValueType *d_y, int iters, void *stream);
 int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
-/* Kernel variant bits (performance experiments; every variant computes the same y).
+/* Kernel variants (performance experiments; every variant computes the same y).
  * Tile kernel: bit 0 = non-temporal streamed loads, bit 1 = non-temporal y stores (default 0).
- * Sweep kernel: bit 0 = non-temporal entry loads, bit 1 = workgroup barrier per iteration,
- * bit 2 = two entry groups per thread per iteration, bit 3 = 2-entry groups instead of 4,
- * bit 4 = software-pipelined entry stream (bits 1-3 ignored); 20/21/22 = 4x2, 4x4, 8x2 entries
- * per thread per barrier. On the packed 12-byte entries (plans built without SPMV_SWEEP_PACKED=0)
- * 15/20/22 = 2/4/8 groups of 2 per barrier, 26-34 = barrier-free waves that may run at most
- * 1-4 iterations ahead of the slowest wave of the workgroup (default 28 = 2 groups, lag 2). */
+ * Sweep kernel, packed entries: 15/20/22 = 2/4/8 entry groups per wave per workgroup barrier;
+ * 26-34 = no barrier, waves run at most 1-4 iterations ahead of the slowest wave of the
+ * workgroup (26: 4 groups lag 1, 27: 4/2, 28: 2/2 = default, 29: 2/4, 30: 2/1, 31: 3/2,
+ * 32: 1/2, 33: 1/4, 34: 2/3). Unpacked entries (a chunk spans >= 65536 columns): 0/1/3/7/15/22
+ * and the default (4 groups of 2 per barrier). */
 int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */

@@ -146,86 +146,6 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
         y[r0 + i] = V(ylds[i]);
 }
 
-// Software-pipelined sweep: the entry stream of group g+1 is loaded while group g's gathers
-// and LDS adds run, so HBM latency is paid once per panel, not once per barrier. Two named
-// register sets (A/B, loop unrolled by two) avoid moves out of registers with loads in
-// flight; gathers are issued BEFORE the next group's loads, so waiting for them (vmcnt counts
-// in issue order) leaves the prefetch in flight. Loads are unconditional with clamped
-// addresses (entry ranges are multiples of 4); out-of-range groups skip their adds. One
-// barrier per group keeps the 16 waves on one column window.
-template <bool NT, typename V>
-struct SweepGroup {
-    u32x4 c;
-    u16x4 r;
-    V v[4];
-    __device__ __forceinline__ void load(const uint32_t *__restrict__ col, const uint16_t *__restrict__ row,
-                                         const V *__restrict__ val, uint64_t e)
-    {
-        c = lds_<NT>(reinterpret_cast<const u32x4 *>(col + e));
-        r = lds_<NT>(reinterpret_cast<const u16x4 *>(row + e));
-        load4<NT>(val, e, v);
-    }
-};
-
-template <typename V, int T, bool NT>
-__global__ __launch_bounds__(T) void k_spmv_sweep_pipe(
-    const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
-    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
-    const V *__restrict__ x, V *__restrict__ y)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
-    const uint32_t p = blockIdx.x;
-    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
-    const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
-    for (uint32_t i = threadIdx.x; i <= R; i += T)
-        ylds[i] = SweepAcc(0);
-    constexpr uint64_t kGroup = 4ull * T;
-    const uint64_t elast = e1 > e0 ? e1 - 4 : e0;  // clamp target: a valid quad of the panel
-    auto at = [&](uint64_t e) { return e < e1 ? e : elast; };
-    uint64_t e = e0 + 4ull * threadIdx.x;
-    SweepGroup<NT, V> A, B;
-    if (e1 > e0)
-        A.load(col, row, val, at(e));
-    __syncthreads();  // LDS zeroed before any add
-    for (uint64_t base = e0; base < e1; base += 2 * kGroup) {
-        // ---- group A (entries e) ----
-        V xa[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            xa[j] = x[A.c[j]];
-        __builtin_amdgcn_sched_barrier(0);  // keep the gathers ahead of the prefetch
-        B.load(col, row, val, at(e + kGroup));
-        {
-            const bool ok = e < e1;  // a clamped (duplicate) quad adds into the scratch slot R
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                atomicAdd(&ylds[ok ? (uint32_t)A.r[j] : R], SweepAcc(A.v[j]) * SweepAcc(xa[j]));
-        }
-        __syncthreads();
-        if (base + kGroup >= e1)
-            break;
-        // ---- group B (entries e + kGroup) ----
-        V xb[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            xb[j] = x[B.c[j]];
-        __builtin_amdgcn_sched_barrier(0);
-        A.load(col, row, val, at(e + 2 * kGroup));
-        {
-            const bool ok = e + kGroup < e1;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                atomicAdd(&ylds[ok ? (uint32_t)B.r[j] : R], SweepAcc(B.v[j]) * SweepAcc(xb[j]));
-        }
-        __syncthreads();
-        e += 2 * kGroup;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < R; i += T)
-        y[r0 + i] = V(ylds[i]);
-}
-
 // Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
 // one u32 base column per 128-entry chunk (one wave instruction of 2-entry lanes). Panels are
 // padded to whole chunks, so the chunk of a wave is wave-uniform and its base is a scalar load.
@@ -305,117 +225,6 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
                 __builtin_amdgcn_s_sleep(1);
             }
         }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < R; i += T)
-        y[r0 + i] = V(ylds[i]);
-}
-
-// Software-pipelined form of k_spmv_sweep_packed. Without it every wave runs
-// entry-load (HBM latency) -> gather (L2 latency) -> LDS add back to back, and the CU holds
-// only 16 waves, so the sweep is bound by Little's law rather than by any pipe. Here the
-// entries of the next stage are loaded while the gathers of this stage are in flight. Vector
-// memory counters retire in issue order; a buffer is refilled only after its adds, so the two
-// buffers alternate (loop unrolled by two) without any register of a pending load being copied
-// at the back edge, and the entries of stage i+1 are in flight while stage i gathers and adds.
-template <typename V, int Q> struct SweepStage {
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    u32x2 w[Q];
-    uint32_t cb[Q];
-    V v[Q][2];
-    bool ok[Q];
-};
-
-template <typename V, int T, int Q, bool NT, int LAG>
-__global__ __launch_bounds__(T) void k_spmv_sweep_packed_pipe(
-    const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
-    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
-    const V *__restrict__ x, V *__restrict__ y)
-{
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
-    const uint32_t p = blockIdx.x;
-    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
-    const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
-    __shared__ uint32_t progress[T / 64];
-    for (uint32_t i = threadIdx.x; i <= R; i += T)
-        ylds[i] = SweepAcc(0);
-    if (threadIdx.x < T / 64)
-        progress[threadIdx.x] = 0;
-    __syncthreads();
-    if (e1 == e0) {
-        for (uint32_t i = threadIdx.x; i < R; i += T)
-            y[r0 + i] = V(0);
-        return;
-    }
-    constexpr uint64_t kGroup = 2ull * T, kStep = Q * kGroup;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane2 = 2u * (threadIdx.x & 63);
-    const uint64_t last_chunk = e1 - 128;
-    const uint32_t nit = (uint32_t)((e1 - e0 + kStep - 1) / kStep);
-
-    auto load = [&](SweepStage<V, Q> &S, uint32_t it) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            uint64_t wbase = e0 + uint64_t(it) * kStep + q * kGroup + 128ull * wave;
-            S.ok[q] = wbase < e1;
-            wbase = S.ok[q] ? wbase : last_chunk;
-            const uint64_t e = wbase + lane2;
-            S.w[q] = lds_<NT>(reinterpret_cast<const u32x2 *>(rc + e));
-            S.cb[q] = cbase[wbase >> 7];
-            __builtin_amdgcn_sched_barrier(0);
-            loadv<NT, 2>(val, e, S.v[q]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };  // (fixed issue order in the prologue and the loop, so the waitcnt states agree)
-    uint32_t iter = 0;
-    auto step = [&](SweepStage<V, Q> &S, uint32_t it_next) {
-        V xv[Q][2];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            xv[q][0] = x[S.cb[q] + (S.w[q].x & 0xFFFFu)];
-            xv[q][1] = x[S.cb[q] + (S.w[q].y & 0xFFFFu)];
-        }
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            atomicAdd(&ylds[S.ok[q] ? (S.w[q].x >> 16) : R], SweepAcc(S.v[q][0]) * SweepAcc(xv[q][0]));
-            atomicAdd(&ylds[S.ok[q] ? (S.w[q].y >> 16) : R], SweepAcc(S.v[q][1]) * SweepAcc(xv[q][1]));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        load(S, it_next);  // refill the consumed buffer (clamped past the end: valid, discarded)
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (LAG == 0) {
-            __syncthreads();
-        } else {
-            ++iter;
-            if ((threadIdx.x & 63) == 0)
-                __hip_atomic_store(&progress[wave], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            for (;;) {
-                const uint32_t lane = threadIdx.x & 63;
-                uint32_t pr = lane < T / 64
-                                  ? __hip_atomic_load(&progress[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                                  : 0xFFFFFFFFu;
-#pragma unroll
-                for (int d = 1; d < T / 64; d <<= 1) {
-                    const uint32_t o = __shfl_xor(pr, d, 64);
-                    pr = o < pr ? o : pr;
-                }
-                if (__builtin_amdgcn_readfirstlane(pr) + LAG >= iter)
-                    break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-    };
-    SweepStage<V, Q> A, B;
-    load(A, 0);
-    load(B, 1);
-    // always both steps (an odd count runs one all-clamped step into the scratch slot): a
-    // conditional second step would make the waitcnt pass assume B's loads may be missing and
-    // drain every load at the loop head
-    for (uint32_t it = 0; it < nit; it += 2) {
-        step(A, it + 2);
-        step(B, it + 3);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < R; i += T)
@@ -561,8 +370,8 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 {
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(SweepAcc);
     const dim3 grid((unsigned)p.npanels), block(T);
-    // variant bits: 0 = non-temporal entry loads, 1 = barrier per iteration,
-    // 2 = two groups per iteration, 3 = groups of 2 entries per thread, 4 = pipelined stream
+    // Unpacked (14-B entries, used when a chunk spans >= 65536 columns): E entries per thread,
+    // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     hipLaunchKernelGGL((k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>), grid, block, lds, s, p.d_s_col, \
                        p.d_s_row, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y)
@@ -570,81 +379,32 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #define PK(Q, LAG)                                                                                  \
     hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, Q, true, LAG>), grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y)
-#define PP(Q, LAG)                                                                                  \
-    hipLaunchKernelGGL((k_spmv_sweep_packed_pipe<ValueType, T, Q, true, LAG>), grid, block, lds, s,      \
-                       p.d_s_col, p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y)
-        // 15/20: Q groups per barrier; 26-34: loose sync with lag; 40-47: pipelined entry loads
+        // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
         case 15: PK(2, 0); break;
         case 20: PK(4, 0); break;
+        case 22: PK(8, 0); break;
         case 26: PK(4, 1); break;
         case 27: PK(4, 2); break;
-        case 28: PK(2, 2); break;
         case 29: PK(2, 4); break;
         case 30: PK(2, 1); break;
         case 31: PK(3, 2); break;
         case 32: PK(1, 2); break;
         case 33: PK(1, 4); break;
         case 34: PK(2, 3); break;
-        case 40: PP(1, 2); break;
-        case 41: PP(2, 2); break;
-        case 42: PP(2, 1); break;
-        case 43: PP(1, 4); break;
-        case 44: PP(2, 0); break;
-        case 45: PP(1, 0); break;
-        case 46: PP(3, 2); break;
-        case 47: PP(2, 4); break;
-        case 48: PP(4, 0); break;
-        case 49: PP(3, 0); break;
-        case 50: PP(4, 2); break;
-        default: PK(8, 0); break;
+        default: PK(2, 2); break;
         }
 #undef PK
-#undef PP
         return;
     }
-    if (p.sweep_variant == 20) {
-        SWEEP(2, 4, true, true);
-        return;
-    }
-    if (p.sweep_variant == 21) {
-        SWEEP(4, 4, true, true);
-        return;
-    }
-    if (p.sweep_variant == 22) {
-        SWEEP(2, 8, true, true);
-        return;
-    }
-    if (p.sweep_variant == 23) {
-        SWEEP(1, 16, true, true);
-        return;
-    }
-    if (p.sweep_variant == 24) {
-        SWEEP(2, 8, true, false);
-        return;
-    }
-    if (p.sweep_variant == 25) {
-        SWEEP(1, 8, true, true);
-        return;
-    }
-    if (p.sweep_variant & 16) {
-        if (p.sweep_variant & 1)
-            hipLaunchKernelGGL((k_spmv_sweep_pipe<ValueType, T, true>), grid, block, lds, s, p.d_s_col, p.d_s_row,
-                               p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
-        else
-            hipLaunchKernelGGL((k_spmv_sweep_pipe<ValueType, T, false>), grid, block, lds, s, p.d_s_col, p.d_s_row,
-                               p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y);
-        return;
-    }
-    switch (p.sweep_variant & 15) {
+    switch (p.sweep_variant) {
     case 0: SWEEP(4, 1, false, false); break;
     case 1: SWEEP(4, 1, false, true); break;
-    case 2: SWEEP(4, 1, true, false); break;
-    case 5: SWEEP(4, 2, false, true); break;
+    case 3: SWEEP(4, 1, true, true); break;
     case 7: SWEEP(4, 2, true, true); break;
-    case 11: SWEEP(2, 1, true, true); break;
     case 15: SWEEP(2, 2, true, true); break;
-    default: SWEEP(4, 1, true, true); break;
+    case 22: SWEEP(2, 8, true, true); break;
+    default: SWEEP(2, 4, true, true); break;  // best unpacked form (0.88 ms on the 10M/160M matrix)
     }
 #undef SWEEP
 }

@@ -27,17 +27,21 @@ def torch():
     return t
 
 
-KERNELS = ["tiles", "tiles_wide", "sweep"]
-KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2}
+KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked"]
+KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2}
 
 
 @pytest.fixture(params=KERNELS)
 def kernel(request, monkeypatch):
     """Plans are built with SPMV_HW_KERNEL forced to each kernel in turn; "tiles_wide" is the
-    tile kernel with 32-bit columns (SPMV_TILE_NARROW=0) instead of per-tile 16-bit offsets."""
+    tile kernel with 32-bit columns (SPMV_TILE_NARROW=0) instead of per-tile offsets and
+    "sweep_unpacked" the sweep on 14-byte entries (SPMV_SWEEP_PACKED=0), the layout used when a
+    chunk of a panel spans >= 65536 columns."""
     monkeypatch.setenv("SPMV_HW_KERNEL", request.param.split("_")[0])
     if request.param == "tiles_wide":
         monkeypatch.setenv("SPMV_TILE_NARROW", "0")
+    if request.param == "sweep_unpacked":
+        monkeypatch.setenv("SPMV_SWEEP_PACKED", "0")
     return request.param
 
 
@@ -62,6 +66,8 @@ def run_device(torch, lib, row_ptr, col, val, x, nr_cols, poison=True, expect_ke
         assert stats["kernel"] == KERNEL_ID[expect_kernel]
         if expect_kernel == "tiles_wide":
             assert not stats["format"] & 1
+        if expect_kernel == "sweep_unpacked":
+            assert not stats["format"] & 2
     return out, stats
 
 
@@ -307,6 +313,55 @@ def test_narrow_tiles_span_limit(torch, monkeypatch, span, narrow):
     y, st = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel="tiles")
     assert st["format"] & 9 == narrow
     check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y, np.float64)
+
+
+PACKED_VARIANTS = [15, 20, 22, 26, 27, 28, 29, 30, 31, 32, 33, 34]
+UNPACKED_VARIANTS = [0, 1, 3, 7, 15, 20, 22]
+
+
+@pytest.mark.parametrize("packed", [True, False])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sweep_variants_agree(torch, monkeypatch, packed, dtype):
+    """Every sweep variant (barrier / loose-sync forms, group counts) computes the same y."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    monkeypatch.setenv("SPMV_SWEEP_PACKED", "1" if packed else "0")
+    lib = spmv_hw.load(dtype)
+    n, z = 200_000, 3_200_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    assert bool(plan.stats()["format"] & 2) == packed
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref = oracle.spmv_gold(row_ptr, c, v, xx)
+    y = torch.empty(n, dtype=x.dtype, device="cuda")
+    for var in (PACKED_VARIANTS if packed else UNPACKED_VARIANTS):
+        y.fill_(float("nan"))
+        plan.set_variant(var)
+        plan.run(x, y)
+        torch.cuda.synchronize()
+        check(row_ptr, c, v, xx, ref, y.cpu().numpy(), dtype)
+    plan.destroy()
+
+
+def test_sweep_falls_back_to_unpacked_entries_on_sparse_panels(torch, monkeypatch):
+    """A panel too sparse for 16-bit column offsets inside a 128-entry chunk (here 16K entries
+    per panel over 10M columns: a chunk spans ~80K columns) keeps the 14-byte entries."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    monkeypatch.delenv("SPMV_SWEEP_PACKED", raising=False)
+    lib = spmv_hw.load(np.float64)
+    n, m = 256_000, 10_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, 16 * n, seed=4)
+    x = spmv_hw.gen_vector(lib, m, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, m)
+    assert plan.stats()["format"] & 2 == 0
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    h = [t.cpu().numpy() for t in (rp, col, val, x, y)]
+    row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
+    check(row_ptr, c, v, xx, oracle.spmv_gold(row_ptr, c, v, xx), yy, np.float64)
+    plan.destroy()
 
 
 def test_auto_kernel_choice(torch, monkeypatch):
