@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
     ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the row-parallel CPU line (the box's CPU share is 16)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
     return ap.parse_args()
@@ -114,7 +116,7 @@ def build_workload(lib, args, world, rank):
     return rp, col, val, x, n, desc
 
 
-def cpu_baseline(lib, rp, col, val, x, y_gpu, reps):
+def cpu_baseline(lib, rp, col, val, x, y_gpu, reps, args_threads=16):
     """Times the oracle's restatement of spmv_gold (1 thread, -O2 -ffp-contract=off) on the
     same matrix in host memory, and checks the full-size GPU result against it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -143,6 +145,30 @@ def cpu_baseline(lib, rp, col, val, x, y_gpu, reps):
             "sample": f"full matrix ({n} rows, {nnz} nnz), median of {len(times)} runs, "
                       f"{t * 1e3:.1f} ms/SpMV, oracle/csr_ref.c spmv_gold, host {model}, "
                       f"nproc {os.cpu_count()}"}
+    # second line: the same restatement row-parallel on host threads (ctypes
+    # releases the GIL; nnz-balanced row slices), labelled as such
+    from concurrent.futures import ThreadPoolExecutor
+    nt = max(1, min(args_threads, os.cpu_count() or 1))
+    bounds = lib.partition_rows(h_rp, nt)
+    y_mt = np.zeros(n, h_val.dtype)
+
+    def part(t):
+        r0, r1 = int(bounds[t]), int(bounds[t + 1])
+        if r1 > r0:
+            oracle.spmv_gold_rows(h_rp, h_col, h_val, h_x, r0, r1, out=y_mt[r0:r1])
+
+    times_mt = []
+    with ThreadPoolExecutor(nt) as ex:
+        for _ in range(max(1, reps)):
+            t0 = time.perf_counter()
+            list(ex.map(part, range(nt)))
+            times_mt.append(time.perf_counter() - t0)
+    t_mt = float(np.median(times_mt))
+    assert np.array_equal(y_mt.view(np.uint8), y.view(np.uint8))  # same rows, same order
+    base["threads_line"] = {"value": round(2.0 * nnz / t_mt / 1e9, 4), "unit": "GFLOP/s", "cores": nt,
+                            "kind": "port", "sample": f"same matrix, row-parallel restatement: {nt} threads "
+                                                      f"over nnz-balanced row slices, median of {len(times_mt)} "
+                                                      f"runs, {t_mt * 1e3:.1f} ms/SpMV"}
     parity = {"max_scaled_err": err, "tol": 1e-6 if h_val.dtype == np.float64 else 1e-4,
               "ref_abs_1e-5_errors": abs_errors, "pass": bool(err <= (1e-6 if h_val.dtype == np.float64 else 1e-4))}
     return base, parity
@@ -291,7 +317,7 @@ def main():
     cpu = None
     parity = None
     if keep_csr:
-        cpu, parity = cpu_baseline(lib, rp, col, val, x, y, args.cpu_reps)
+        cpu, parity = cpu_baseline(lib, rp, col, val, x, y, args.cpu_reps, args.cpu_threads)
 
     if rank == 0:
         out = {
