@@ -30,6 +30,7 @@ for s in $STEPS; do
     banded) run bench_banded 300 python bench.py --workload banded ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
     calib) run calib 300 tools/hbm_calib ;;
+    strong) run strong 600 python tools/strong_slices.py ${STRONG_ARGS:-} ;;
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
               SPMV_BENCH_BACKEND=gloo run rehearse_strong 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --scaling strong ;;
     ab) run ab 600 python tools/ab_variants.py ;;

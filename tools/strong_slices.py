@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Config 4 (strong scaling) rehearsed on ONE GPU: for N in 1,2,4,8 the rank slices of the
+10M x 10M / 160M-nnz power-law matrix (nnz-balanced, exactly as bench.py --scaling strong cuts
+them) are built and timed one after another; the slowest slice is the compute-only step time of
+an N-GPU run. Prints one JSON line per N (kernel ms of the slowest slice, implied aggregate
+GFLOP/s and speed-up vs N=1). The y exchange is not included (bench.py reports it per mode).
+Usage: strong_slices.py [--ns 1,2,4,8] [--slices all|ends] [--dtype f64|f32]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "spmv-fpga_amd")]
+import torch  # noqa: E402
+
+import spmv_dist  # noqa: E402
+import spmv_hw  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--nnz", type=int, default=160_000_000)
+    ap.add_argument("--dtype", default="f64")
+    ap.add_argument("--slices", default="ends", help="'all' slices, or first+last only")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    dtype = np.float64 if a.dtype == "f64" else np.float32
+    lib = spmv_hw.load(dtype)
+    n, z = a.rows, a.nnz
+    rp_full, _ = lib.powerlaw_row_ptr(n, z, 65536, 4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    base = None
+    for N in [int(v) for v in a.ns.split(",")]:
+        b = lib.partition_rows(rp_full, N)
+        ranks = range(N) if a.slices == "all" or N <= 2 else (0, N - 1)
+        worst, per = 0.0, {}
+        for r in ranks:
+            r0, r1 = spmv_dist.row_slice(b, r)
+            rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4, row_begin=r0, row_end=r1)
+            plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+            del rp, col, val
+            y = torch.empty(r1 - r0, dtype=x.dtype, device="cuda")
+            for _ in range(3):
+                plan.run(x, y)
+            plan.set_timing(True)
+            for _ in range(a.reps):
+                plan.run(x, y)
+            ms, _, _ = plan.timing()
+            st = plan.stats()
+            per[r] = {"rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "ms": round(ms, 5),
+                      "panels": st["nr_tiles"]}
+            worst = max(worst, ms)
+            plan.destroy()
+            torch.cuda.empty_cache()
+        gflops = 2.0 * z / (worst * 1e-3) / 1e9
+        if base is None:
+            base = worst
+        print(json.dumps({"n_gpus": N, "dtype": a.dtype, "slowest_slice_ms": round(worst, 5),
+                          "aggregate_GFLOPs": round(gflops, 1), "speedup_vs_1": round(base / worst, 3),
+                          "slices": per}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
