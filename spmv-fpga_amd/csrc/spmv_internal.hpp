@@ -73,13 +73,15 @@ struct spmv_plan {
 
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
+    uint64_t nunits = 0;               // workgroups of a launch = npanels * sweep_split
+    uint32_t sweep_split = 1;          // pieces per panel (column ranges); > 1 adds with atomics
     uint32_t panel_rmax = 0;
     int sweep_threads = spmvhw::kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)
     uint32_t *d_s_col = nullptr;
     uint16_t *d_s_row = nullptr;
     ValueType *d_s_val = nullptr;
     uint32_t *d_panel_row = nullptr;
-    uint32_t *d_panel_ent = nullptr;
+    uint32_t *d_unit_ent = nullptr;
     uint32_t *d_s_cbase = nullptr;   // packed form: base column per 128-entry chunk
     bool sweep_packed = false;
     bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)

@@ -15,7 +15,9 @@
 //   s_col u32[ent_pad]  column of each entry, panels contiguous, ascending column per panel
 //   s_row u16[ent_pad]  row inside the panel (padding entries use the scratch slot R_p)
 //   s_val V[ent_pad]    value
-//   panel_row u32[P+1]  row range of panel p; panel_ent u32[P+1] entry range (multiples of 128)
+//   panel_row u32[P+1]  row range of panel p
+//   unit_ent u32[U+1]   entry range of work unit u = (panel u / split, piece u % split); with
+//                       split = 1 the panel's whole (128-padded) entry range
 // Packed form (default when every 128-entry chunk spans < 65536 columns, 12 B/entry):
 //   s_col u32 holds (row_in_panel << 16) | (column - s_cbase[chunk]); s_row is dropped; inside a
 //   chunk, word 2l+j holds entry 64j+l (k_sweep_lane_order) so one gather instruction covers 64
@@ -90,22 +92,41 @@ __device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o
     }
 }
 
+// A unit's y: stored when the panel is one unit; with split pieces (split > 1) each piece holds
+// a partial sum over its column range and adds it with a global fp64/fp32 atomic (y is zeroed
+// before the launch). Rows without entries in the piece (partial exactly 0) add nothing.
+template <typename V, int T>
+__device__ __forceinline__ void write_panel(const SweepAcc *__restrict__ ylds, uint32_t R, V *__restrict__ y,
+                                            uint32_t split)
+{
+    if (split == 1) {
+        for (uint32_t i = threadIdx.x; i < R; i += T)
+            y[i] = V(ylds[i]);
+    } else {
+        for (uint32_t i = threadIdx.x; i < R; i += T) {
+            const SweepAcc v = ylds[i];
+            if (v != SweepAcc(0))
+                atomicAdd(&y[i], V(v));
+        }
+    }
+}
+
 // E entries per thread per workgroup iteration, Q such groups per iteration; SYNC: barrier after
 // every iteration so the 16 waves stay on one column window; NT: non-temporal entry loads.
 // Entry ranges of a panel are multiples of 4, so whole E-groups are always valid.
 template <typename V, int T, int E, int Q, bool SYNC, bool NT>
 __global__ __launch_bounds__(T) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
-    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent, uint32_t split,
     const V *__restrict__ x, V *__restrict__ y)
 {
     typedef typename EntryVec<E>::C CV;
     typedef typename EntryVec<E>::R RV;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
-    const uint32_t p = blockIdx.x;
+    const uint32_t p = blockIdx.x / split;  // unit = (panel, piece of its column-sorted entries)
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
-    const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
+    const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     for (uint32_t i = threadIdx.x; i <= R; i += T)
         ylds[i] = SweepAcc(0);
     __syncthreads();
@@ -142,8 +163,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
             __syncthreads();
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < R; i += T)
-        y[r0 + i] = V(ylds[i]);
+    write_panel<V, T>(ylds, R, y + r0, split);
 }
 
 // Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
@@ -155,15 +175,15 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
 template <typename V, int T, int Q, bool NT, int LAG = 0>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
-    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_ent,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent, uint32_t split,
     const V *__restrict__ x, V *__restrict__ y)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
-    const uint32_t p = blockIdx.x;
+    const uint32_t p = blockIdx.x / split;  // unit = (panel, piece of its column-sorted entries)
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
-    const uint64_t e0 = panel_ent[p], e1 = panel_ent[p + 1];
+    const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     __shared__ uint32_t progress[T / 64];
     for (uint32_t i = threadIdx.x; i <= R; i += T)
         ylds[i] = SweepAcc(0);
@@ -227,8 +247,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < R; i += T)
-        y[r0 + i] = V(ylds[i]);
+    write_panel<V, T>(ylds, R, y + r0, split);
 }
 
 // chunk c of 128 entries: base = min column; fails the plan's packing when the span >= 65536
@@ -369,16 +388,16 @@ template <int T>
 static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
 {
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(SweepAcc);
-    const dim3 grid((unsigned)p.npanels), block(T);
+    const dim3 grid((unsigned)p.nunits), block(T);
     // Unpacked (14-B entries, used when a chunk spans >= 65536 columns): E entries per thread,
     // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     hipLaunchKernelGGL((k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>), grid, block, lds, s, p.d_s_col, \
-                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y)
+                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, d_x, d_y)
     if (p.sweep_packed) {
 #define PK(Q, LAG)                                                                                  \
     hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, Q, true, LAG>), grid, block, lds, s, p.d_s_col, \
-                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_panel_ent, d_x, d_y)
+                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, d_x, d_y)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
         case 15: PK(2, 0); break;
@@ -413,6 +432,11 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
 {
     if (p.npanels == 0)
         return hipSuccess;
+    if (p.sweep_split > 1) {  // pieces add their partial sums into a zeroed y
+        const hipError_t e = hipMemsetAsync(d_y, 0, size_t(p.nr_rows) * sizeof(ValueType), s);
+        if (e != hipSuccess)
+            return e;
+    }
     switch (p.sweep_threads) {
     case 256: launch_sweep_t<256>(p, d_x, d_y, s); break;
     case 512: launch_sweep_t<512>(p, d_x, d_y, s); break;
@@ -421,8 +445,14 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
     return hipGetLastError();
 }
 
-// Host: panel boundaries (nnz-balanced, <= rmax rows each, a multiple of the CU count when
-// possible), then the device sort + scatter.
+// Host: panel boundaries (nnz-balanced, <= rmax rows each), then the device sort + scatter.
+// Work units: when the slice has at least one panel per resident workgroup, panels are rounded
+// to whole rounds of workgroups and each panel is one unit. When it has fewer (a slice of fewer
+// than ~5M rows), the panels keep their full LDS size and each is cut into `split` pieces of
+// whole chunks of its column-sorted entries (contiguous column ranges, equal entry counts) --
+// the reference's 2-D blocking (row slices x column blocks, csr_hw.cpp:25-76) with the column
+// blocks sized by work. Denser panels touch fewer x lines per non-zero; the pieces' partial
+// sums are added with global atomics (env SPMV_SWEEP_SPLIT=0 keeps the smaller-panel form).
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s)
 {
@@ -438,9 +468,13 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             cus = prop.multiProcessorCount;
     }
     cus *= 1024 / p.sweep_threads;  // resident workgroups per round
+    const char *senv = std::getenv("SPMV_SWEEP_SPLIT");
+    const bool allow_split = !(senv && senv[0] == '0');
+    bool split_mode = false;
     std::vector<uint32_t> prow;
     for (uint64_t P = std::max<uint64_t>(1, (n + rmax - 1) / rmax);; ++P) {
-        if (P > 1 && P % cus)
+        split_mode = allow_split && P < (uint64_t)cus && nnz >= 4ull * kSweepChunk * (uint64_t)cus;
+        if (!split_mode && P > 1 && P % cus)
             P = (P + cus - 1) / cus * cus;  // whole rounds of workgroups
         P = std::min<uint64_t>(P, std::max<uint64_t>(n, 1));
         prow.assign(1, 0);
@@ -481,6 +515,17 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     p.npanels = P;
     p.panel_rmax = rmax_used;
     p.ent_pad = poff[P];
+    // work units: `split` pieces of whole chunks per panel
+    const uint32_t split = split_mode ? std::max<uint32_t>(1, (uint32_t)cus / P) : 1;
+    std::vector<uint32_t> uent((size_t)P * split + 1);
+    for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
+        for (uint32_t t = 0; t < split; ++t)
+            uent[(size_t)q * split + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / split));
+    }
+    uent[(size_t)P * split] = poff[P];
+    p.sweep_split = split;
+    p.nunits = (uint64_t)P * split;
 
     // bucket shift so that P * buckets fits 32-bit keys
     uint32_t shift = 0;
@@ -492,9 +537,9 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         ++end_bit;
 
     SPMV_TRY(hipMalloc((void **)&p.d_panel_row, (P + 1) * 4));
-    SPMV_TRY(hipMalloc((void **)&p.d_panel_ent, (P + 1) * 4));
+    SPMV_TRY(hipMalloc((void **)&p.d_unit_ent, uent.size() * 4));
     SPMV_TRY(hipMemcpyAsync(p.d_panel_row, prow.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
-    SPMV_TRY(hipMemcpyAsync(p.d_panel_ent, poff.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipMemcpyAsync(p.d_unit_ent, uent.data(), uent.size() * 4, hipMemcpyHostToDevice, s));
     SPMV_TRY(hipMalloc((void **)&p.d_s_col, std::max<uint64_t>(p.ent_pad, 4) * 4));
     SPMV_TRY(hipMalloc((void **)&p.d_s_row, std::max<uint64_t>(p.ent_pad, 4) * 2));
     SPMV_TRY(hipMalloc((void **)&p.d_s_val, std::max<uint64_t>(p.ent_pad, 4) * sizeof(ValueType)));

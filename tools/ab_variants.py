@@ -47,6 +47,9 @@ def main():
                 if kern.endswith("U"):
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_PACKED"] = "0"
+                if kern.endswith("S"):  # sweep without split panels (smaller panels instead)
+                    kern = kern[:-1]
+                    os.environ["SPMV_SWEEP_SPLIT"] = "0"
                 if kern.endswith("H"):  # tile kernel with at most 16-bit column offsets
                     kern = kern[:-1]
                     os.environ["SPMV_TILE_NARROW"] = "16"
@@ -64,6 +67,7 @@ def main():
                 os.environ.pop("SPMV_SWEEP_PACKED", None)
                 os.environ.pop("SPMV_SWEEP_LANE_ORDER", None)
                 os.environ.pop("SPMV_TILE_NARROW", None)
+                os.environ.pop("SPMV_SWEEP_SPLIT", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
