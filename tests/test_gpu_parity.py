@@ -349,6 +349,7 @@ def test_sweep_falls_back_to_unpacked_entries_on_sparse_panels(torch, monkeypatc
     per panel over 10M columns: a chunk spans ~80K columns) keeps the 14-byte entries."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     monkeypatch.delenv("SPMV_SWEEP_PACKED", raising=False)
+    monkeypatch.setenv("SPMV_SWEEP_SPLIT", "0")  # 256 small panels, not 13 full ones in pieces
     lib = spmv_hw.load(np.float64)
     n, m = 256_000, 10_000_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, 16 * n, seed=4)
@@ -362,6 +363,35 @@ def test_sweep_falls_back_to_unpacked_entries_on_sparse_panels(torch, monkeypatc
     row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
     check(row_ptr, c, v, xx, oracle.spmv_gold(row_ptr, c, v, xx), yy, np.float64)
     plan.destroy()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sweep_split_pieces_match_oracle(torch, monkeypatch, dtype):
+    """A strong-scaling-like slice (few rows, wide x): full-size panels cut into column pieces
+    whose partial sums meet in y through global atomics; also the same plan forced unsplit."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    lib = spmv_hw.load(dtype)
+    n_full, z_full = 10_000_000, 160_000_000
+    r0, r1 = 0, 1_250_000  # rank 0 of 8 (row slice of the 10M/160M matrix, rows only)
+    ys = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("SPMV_SWEEP_SPLIT", split)
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n_full, n_full, z_full, seed=4, row_begin=r0, row_end=r1)
+        x = spmv_hw.gen_vector(lib, n_full, seed=6)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n_full)
+        st = plan.stats()
+        y = torch.full((r1 - r0,), float("nan"), dtype=x.dtype, device="cuda")
+        plan.run(x, y)
+        plan.run(x, y)  # y is re-zeroed by every run: no accumulation across calls
+        torch.cuda.synchronize()
+        ys[split] = (st["nr_tiles"], y.cpu().numpy())
+        plan.destroy()
+    assert ys["1"][0] < 256 and ys["0"][0] == 256  # pieces of ~62 full panels vs 256 small ones
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref = oracle.spmv_gold(row_ptr, c, v, xx)
+    for split, (_, y) in ys.items():
+        check(row_ptr, c, v, xx, ref, y, dtype)
 
 
 def test_auto_kernel_choice(torch, monkeypatch):
