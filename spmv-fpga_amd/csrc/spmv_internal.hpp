@@ -74,7 +74,8 @@ struct spmv_plan {
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
     uint64_t nunits = 0;               // workgroups of a launch = npanels * sweep_split
-    uint32_t sweep_split = 1;          // pieces per panel (column ranges); > 1 adds with atomics
+    uint32_t sweep_split = 1;          // pieces per panel (column ranges); > 1: partials + combine
+    double *d_part = nullptr;          // split > 1: nunits x (panel_rmax + 1) fp64 partial sums
     uint32_t panel_rmax = 0;
     int sweep_threads = spmvhw::kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)
     uint32_t *d_s_col = nullptr;

@@ -92,23 +92,39 @@ __device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o
     }
 }
 
-// A unit's y: stored when the panel is one unit; with split pieces (split > 1) each piece holds
-// a partial sum over its column range and adds it with a global fp64/fp32 atomic (y is zeroed
-// before the launch). Rows without entries in the piece (partial exactly 0) add nothing.
+// A unit's y: stored when the panel is one unit; with split pieces (split > 1) each piece
+// stores its fp64 partial sums (its column range) into part[unit * stride + i], and
+// k_sweep_combine adds the pieces of every row in piece order (deterministic, one rounding).
 template <typename V, int T>
 __device__ __forceinline__ void write_panel(const SweepAcc *__restrict__ ylds, uint32_t R, V *__restrict__ y,
-                                            uint32_t split)
+                                            uint32_t split, SweepAcc *__restrict__ part, uint32_t stride)
 {
     if (split == 1) {
         for (uint32_t i = threadIdx.x; i < R; i += T)
             y[i] = V(ylds[i]);
     } else {
-        for (uint32_t i = threadIdx.x; i < R; i += T) {
-            const SweepAcc v = ylds[i];
-            if (v != SweepAcc(0))
-                atomicAdd(&y[i], V(v));
-        }
+        SweepAcc *dst = part + (uint64_t)blockIdx.x * stride;
+        for (uint32_t i = threadIdx.x; i < R; i += T)
+            dst[i] = ylds[i];
     }
+}
+
+// y[r0 + i] = sum over the panel's pieces s (in order) of part[(p * split + s) * stride + i]
+template <typename V>
+__global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restrict__ panel_row, uint32_t split,
+                                                       const SweepAcc *__restrict__ part, uint32_t stride,
+                                                       V *__restrict__ y)
+{
+    const uint32_t p = blockIdx.y;
+    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= R)
+        return;
+    const SweepAcc *src = part + (uint64_t)p * split * stride + i;
+    SweepAcc acc = src[0];
+    for (uint32_t t = 1; t < split; ++t)
+        acc += src[(uint64_t)t * stride];
+    y[r0 + i] = V(acc);
 }
 
 // E entries per thread per workgroup iteration, Q such groups per iteration; SYNC: barrier after
@@ -118,7 +134,7 @@ template <typename V, int T, int E, int Q, bool SYNC, bool NT>
 __global__ __launch_bounds__(T) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent, uint32_t split,
-    const V *__restrict__ x, V *__restrict__ y)
+    SweepAcc *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef typename EntryVec<E>::C CV;
     typedef typename EntryVec<E>::R RV;
@@ -163,7 +179,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
             __syncthreads();
     }
     __syncthreads();
-    write_panel<V, T>(ylds, R, y + r0, split);
+    write_panel<V, T>(ylds, R, y + r0, split, part, stride);
 }
 
 // Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
@@ -176,7 +192,7 @@ template <typename V, int T, int Q, bool NT, int LAG = 0>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent, uint32_t split,
-    const V *__restrict__ x, V *__restrict__ y)
+    SweepAcc *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -247,7 +263,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         }
     }
     __syncthreads();
-    write_panel<V, T>(ylds, R, y + r0, split);
+    write_panel<V, T>(ylds, R, y + r0, split, part, stride);
 }
 
 // chunk c of 128 entries: base = min column; fails the plan's packing when the span >= 65536
@@ -393,11 +409,11 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     hipLaunchKernelGGL((k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>), grid, block, lds, s, p.d_s_col, \
-                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, d_x, d_y)
+                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, p.d_part, p.panel_rmax + 1, d_x, d_y)
     if (p.sweep_packed) {
 #define PK(Q, LAG)                                                                                  \
     hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, Q, true, LAG>), grid, block, lds, s, p.d_s_col, \
-                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, d_x, d_y)
+                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, p.d_part, p.panel_rmax + 1, d_x, d_y)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
         case 15: PK(2, 0); break;
@@ -432,15 +448,15 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
 {
     if (p.npanels == 0)
         return hipSuccess;
-    if (p.sweep_split > 1) {  // pieces add their partial sums into a zeroed y
-        const hipError_t e = hipMemsetAsync(d_y, 0, size_t(p.nr_rows) * sizeof(ValueType), s);
-        if (e != hipSuccess)
-            return e;
-    }
     switch (p.sweep_threads) {
     case 256: launch_sweep_t<256>(p, d_x, d_y, s); break;
     case 512: launch_sweep_t<512>(p, d_x, d_y, s); break;
     default: launch_sweep_t<1024>(p, d_x, d_y, s); break;
+    }
+    if (p.sweep_split > 1) {
+        const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
+        hipLaunchKernelGGL((k_sweep_combine<ValueType>), grid, dim3(256), 0, s, p.d_panel_row, p.sweep_split,
+                           p.d_part, p.panel_rmax + 1, d_y);
     }
     return hipGetLastError();
 }
@@ -451,8 +467,9 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
 // than ~5M rows), the panels keep their full LDS size and each is cut into `split` pieces of
 // whole chunks of its column-sorted entries (contiguous column ranges, equal entry counts) --
 // the reference's 2-D blocking (row slices x column blocks, csr_hw.cpp:25-76) with the column
-// blocks sized by work. Denser panels touch fewer x lines per non-zero; the pieces' partial
-// sums are added with global atomics (env SPMV_SWEEP_SPLIT=0 keeps the smaller-panel form).
+// blocks sized by work. Denser panels touch fewer x lines per non-zero; the pieces' fp64
+// partial sums go to a scratch array and k_sweep_combine adds them per row in piece order
+// (env SPMV_SWEEP_SPLIT=0 keeps the smaller-panel form).
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s)
 {
@@ -468,19 +485,20 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             cus = prop.multiProcessorCount;
     }
     cus *= 1024 / p.sweep_threads;  // resident workgroups per round
+    // env SPMV_SWEEP_SPLIT: 0 = never split, 2 = split whenever >= 2 pieces fit, else heuristic
     const char *senv = std::getenv("SPMV_SWEEP_SPLIT");
     const bool allow_split = !(senv && senv[0] == '0');
+    const bool force_split = senv && senv[0] == '2';
     bool split_mode = false;
     std::vector<uint32_t> prow;
     for (uint64_t P = std::max<uint64_t>(1, (n + rmax - 1) / rmax);; ++P) {
         {
             // pieces pay when the slice fills at most half the workgroups with full panels and
-            // the partial sums (split * n values, added with memory-side atomics at ~1.3 TB/s)
-            // stay small next to the entry stream (measured: strong-scaling slices of the
-            // 10M/160M matrix gain 5-9 %; a 1M-row matrix with x in L2 range loses 8 %)
+            // the partial sums (split * n fp64 values, written once and read once by the
+            // combine) stay small next to the entry stream
             const uint64_t S = P ? (uint64_t)cus / P : 0;
             split_mode = allow_split && S >= 2 && P * S * 10 >= (uint64_t)cus * 9 &&
-                         S * n * sizeof(ValueType) * 5 <= nnz * (4 + sizeof(ValueType));
+                         (force_split || S * n * sizeof(ValueType) * 5 <= nnz * (4 + sizeof(ValueType)));
         }
         if (!split_mode && P > 1 && P % cus)
             P = (P + cus - 1) / cus * cus;  // whole rounds of workgroups
@@ -534,6 +552,8 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     uent[(size_t)P * split] = poff[P];
     p.sweep_split = split;
     p.nunits = (uint64_t)P * split;
+    if (split > 1)
+        SPMV_TRY(hipMalloc((void **)&p.d_part, p.nunits * (uint64_t(rmax_used) + 1) * sizeof(SweepAcc)));
 
     // bucket shift so that P * buckets fits 32-bit keys
     uint32_t shift = 0;

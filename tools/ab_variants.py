@@ -50,6 +50,9 @@ def main():
                 if kern.endswith("S"):  # sweep without split panels (smaller panels instead)
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_SPLIT"] = "0"
+                if kern.endswith("F"):  # sweep with split panels whenever they fit
+                    kern = kern[:-1]
+                    os.environ["SPMV_SWEEP_SPLIT"] = "2"
                 if kern.endswith("H"):  # tile kernel with at most 16-bit column offsets
                     kern = kern[:-1]
                     os.environ["SPMV_TILE_NARROW"] = "16"
