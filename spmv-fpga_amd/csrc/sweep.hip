@@ -495,10 +495,12 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         {
             // pieces pay when the slice fills at most half the workgroups with full panels and
             // the partial sums (split * n fp64 values, written once and read once by the
-            // combine) stay small next to the entry stream
+            // combine) stay below 0.6x the entry stream. Measured (profiles/): a 1M-row
+            // power-law matrix 14 % faster (partials 0.42x the entries), the N = 8 slice of
+            // the 10M/160M matrix 18 % (0.33x), a 300K-row matrix 25 % slower (1.4x)
             const uint64_t S = P ? (uint64_t)cus / P : 0;
             split_mode = allow_split && S >= 2 && P * S * 10 >= (uint64_t)cus * 9 &&
-                         (force_split || S * n * sizeof(ValueType) * 5 <= nnz * (4 + sizeof(ValueType)));
+                         (force_split || 2 * S * n * sizeof(SweepAcc) * 5 <= 3 * nnz * (4 + sizeof(ValueType)));
         }
         if (!split_mode && P > 1 && P % cus)
             P = (P + cus - 1) / cus * cus;  // whole rounds of workgroups
