@@ -368,7 +368,7 @@ def test_sweep_falls_back_to_unpacked_entries_on_sparse_panels(torch, monkeypatc
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_sweep_split_pieces_match_oracle(torch, monkeypatch, dtype):
     """A strong-scaling-like slice (few rows, wide x): full-size panels cut into column pieces
-    whose partial sums meet in y through global atomics; also the same plan forced unsplit."""
+    whose fp64 partial sums k_sweep_combine adds per row; also the same plan forced unsplit."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     lib = spmv_hw.load(dtype)
     n_full, z_full = 10_000_000, 160_000_000
@@ -382,7 +382,7 @@ def test_sweep_split_pieces_match_oracle(torch, monkeypatch, dtype):
         st = plan.stats()
         y = torch.full((r1 - r0,), float("nan"), dtype=x.dtype, device="cuda")
         plan.run(x, y)
-        plan.run(x, y)  # y is re-zeroed by every run: no accumulation across calls
+        plan.run(x, y)  # every run overwrites y: no accumulation across calls
         torch.cuda.synchronize()
         ys[split] = (st["nr_tiles"], y.cpu().numpy())
         plan.destroy()
