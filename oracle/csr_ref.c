@@ -14,7 +14,11 @@
  *   - an independent numpy restatement of spmv_gold, bit-exact on every fixture;
  *   - the reference's own self-check (main.cpp:77-82): the restated FPGA arithmetic order
  *     (spmv.cpp:66-104 + csr_hw.cpp:1531-1565) must pass verification (abs 1e-5) against
- *     spmv_gold on every fixture, for every valid (CU, VF).
+ *     spmv_gold on every fixture, for every valid (CU, VF);
+ *   - the only known answers the reference itself holds, its diagrams (images/1_matrix.svg,
+ *     2_csr.svg, 3_hw_representation_v3.svg, transcribed into
+ *     tests/golden/reference_diagram_kat.json): the reader gives the diagram's CSR and the
+ *     restated packed format (oracle.py pack_hw_submatrix) gives its bus words.
  *
  * Build: gcc -O2 -ffp-contract=off (no FMA, like the reference's -O2 build without -march),
  * -DDOUBLE=1 -> liboracle_f64.so, -DDOUBLE=0 -> liboracle_f32.so (oracle/Makefile).

@@ -130,5 +130,62 @@ def scaled_error(row_ptr, col, val, x, y_ref, y_test) -> float:
     return float(np.max(diff[~zero] / absax[~zero]))
 
 
+def block_matrix(row_ptr, col, val, thres_l: int, thres_h: int, vf: int):
+    """csr_hw.cpp:190-265 (create_block_matrix) for one column block [thres_l, thres_h]:
+    the non-empty rows of the block only, columns rebased to thres_l, every row zero-padded
+    (col 0, value 0) to a multiple of `vf`. Returns (row_ptr, col, val) of the block
+    (without the trailing pad rows that only the last CU carries, csr_hw.cpp:246-255)."""
+    rp_out, c_out, v_out = [0], [], []
+    for i in range(len(row_ptr) - 1):
+        k = [j for j in range(int(row_ptr[i]), int(row_ptr[i + 1])) if thres_l <= int(col[j]) <= thres_h]
+        if not k:
+            continue
+        c_out += [int(col[j]) - thres_l for j in k]
+        v_out += [val[j] for j in k]
+        pad = (-len(k)) % vf
+        c_out += [0] * pad
+        v_out += [val.dtype.type(0)] * pad
+        rp_out.append(rp_out[-1] + len(k) + pad)
+    return (np.array(rp_out, np.uint32), np.array(c_out, np.uint32), np.array(v_out, val.dtype))
+
+
+def pack_hw_submatrix(row_ptr, col, val):
+    """csr_hw.cpp:270-318 (generate_balanced_hw_submatrix) for one CU's rows of one block:
+    128-bit bus words in groups [C, V, V, V, V] (fp64) or [C, V, V] (fp32), util.h:61-67.
+    Field k of a C word holds the column in bits [16k, 16k+14] and the last-element-of-row
+    flag in bit 16k+15 (8 fields per word); lane k of a V word holds value k in bits
+    [W*k, W*k+W-1]. Returns uint64 array (words, 2) = (bits 0-63, bits 64-127)."""
+    w = val.dtype.itemsize * 8
+    ratio_v = 128 // w              # values per V word
+    ratio_col_val = 8 // ratio_v + 1  # one C word per 8 entries, then 8/ratio_v V words
+    z = len(col)
+    words = [0] * max(1, -(-z // 8) * ratio_col_val)
+    c_i, v_i, c_cp, v_cp = 0, 1, 0, 0
+    e = 0
+    for i in range(len(row_ptr) - 1):
+        n_row = int(row_ptr[i + 1]) - int(row_ptr[i])
+        for k in range(n_row):
+            field = (int(col[e]) & 0x7FFF) | ((1 << 15) if k == n_row - 1 else 0)
+            words[c_i] |= field << (16 * c_cp)
+            c_cp += 1
+            if c_cp == 8:
+                c_i += ratio_col_val
+                c_cp = 0
+            bits = int(np.array([val[e]], val.dtype).view(np.uint64 if w == 64 else np.uint32)[0])
+            words[v_i] |= bits << (w * v_cp)
+            v_cp += 1
+            if v_cp == ratio_v:
+                v_i += 1
+                if v_i % ratio_col_val == 0:
+                    v_i += 1
+                v_cp = 0
+            e += 1
+    out = np.zeros((len(words), 2), np.uint64)
+    for j, wd in enumerate(words):
+        out[j, 0] = wd & 0xFFFFFFFFFFFFFFFF
+        out[j, 1] = wd >> 64
+    return out
+
+
 def _c(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)

@@ -2,8 +2,9 @@
 
 Parity status of the oracle: "parity unpinned" (the reference cannot be built here, it ships no
 fixtures). What pins it: glibc rand() known answers recorded in SURVEY.md §8(a3), an independent
-numpy restatement (bit-exact), and the reference's own self-check (main.cpp:77-82) applied to
-the restated FPGA arithmetic order.
+numpy restatement (bit-exact), the reference's own self-check (main.cpp:77-82) applied to
+the restated FPGA arithmetic order, and the known answers of the reference's diagrams
+(images/*.svg -> tests/golden/reference_diagram_kat.json).
 """
 import os
 
@@ -135,3 +136,80 @@ def test_scaled_error_metric():
     assert oracle.scaled_error(row_ptr, col, val, x, y, y) == 0.0
     assert oracle.scaled_error(row_ptr, col, val, x, y, y + np.array([1e-9, 0, 0])) == pytest.approx(5e-10)
     assert oracle.scaled_error(row_ptr, col, val, x, y, y + np.array([0, 1e-30, 0])) == float("inf")
+
+
+# ---- known answers from the reference's own diagrams (tests/golden/reference_diagram_kat.json) ----
+def _kat():
+    import json
+    with open(os.path.join(GOLDEN, "reference_diagram_kat.json")) as f:
+        return json.load(f)
+
+
+def _kat_csr(tmp_path, dtype):
+    """The diagram's 4x4 matrix with a..h = 1..8, written in the reference's text format and
+    read back through the oracle's restatement of the reader."""
+    kat = _kat()
+    sym = {c: float(i + 1) for i, c in enumerate("abcdefgh")}
+    p = tmp_path / "diagram.mtx"
+    ent = kat["matrix_4x4"]["entries"]
+    p.write_text("4 4 %d\n" % len(ent) + "".join(f"{r + 1} {c + 1} {sym[v]}\n" for r, c, v in ent))
+    _, _, rp, col, val, _ = oracle.read_csr(str(p), dtype)
+    return kat, sym, rp, col, val
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_reader_reproduces_reference_csr_diagram(tmp_path, dtype):
+    """2_csr.svg: row_ptr / col_idx / values of the 1_matrix.svg example."""
+    kat, sym, rp, col, val = _kat_csr(tmp_path, dtype)
+    assert rp.tolist() == kat["csr"]["row_ptr"]
+    assert col.tolist() == kat["csr"]["col_idx"]
+    assert val.tolist() == [sym[v] for v in kat["csr"]["values"]]
+
+
+def test_packed_format_reproduces_reference_hw_diagram(tmp_path):
+    """3_hw_representation_v3.svg (fp64, one block, one CU, no row padding): the C word's
+    15-bit columns and last-of-row flags, and the order of the values in the V words."""
+    kat, sym, rp, col, val = _kat_csr(tmp_path, np.float64)
+    brp, bcol, bval = oracle.block_matrix(rp, col, val, 0, 3, vf=1)
+    words = oracle.pack_hw_submatrix(brp, bcol, bval)
+    assert words.shape == (5, 2)  # one [C, V, V, V, V] group for 8 entries
+    c = int(words[0, 0]) | (int(words[0, 1]) << 64)
+    fields = [(c >> (16 * k)) & 0xFFFF for k in range(8)]
+    assert [f & 0x7FFF for f in fields] == kat["hw_v3"]["fields_col"]
+    assert [f >> 15 for f in fields] == kat["hw_v3"]["fields_row_end"]
+    for j, (lo, hi) in enumerate(kat["hw_v3"]["value_words"]):
+        got = words[1 + j].view(np.float64).tolist()
+        assert got == [sym[lo], sym[hi]]
+
+
+@pytest.mark.parametrize("vf", [2, 4])
+def test_packed_format_row_padding_and_fpga_order(tmp_path, vf):
+    """With VF > 1 every row is padded to a multiple of VF (create_block_matrix) and the
+    flag sits on the padded row's last lane; decoding the words and summing in the FPGA
+    order reproduces oracle.spmv_fpga_order on the diagram's matrix."""
+    _, _, rp, col, val = _kat_csr(tmp_path, np.float64)
+    brp, bcol, bval = oracle.block_matrix(rp, col, val, 0, 3, vf=vf)
+    assert np.all(np.diff(brp.astype(np.int64)) % vf == 0)
+    words = oracle.pack_hw_submatrix(brp, bcol, bval)
+    z = int(brp[-1])
+    cols, flags, vals = [], [], []
+    for g in range(-(-z // 8)):
+        c = int(words[5 * g, 0]) | (int(words[5 * g, 1]) << 64)
+        cols += [(c >> (16 * k)) & 0x7FFF for k in range(8)]
+        flags += [(c >> (16 * k + 15)) & 1 for k in range(8)]
+        vals += words[5 * g + 1:5 * g + 5].view(np.float64).reshape(-1).tolist()
+    cols, flags, vals = cols[:z], flags[:z], vals[:z]
+    assert [i for i, f in enumerate(flags) if f] == [int(e) - 1 for e in brp[1:]]
+    x = np.arange(1.0, 5.0)
+    y = np.zeros(4)
+    acc, r = 0.0, 0
+    for g in range(0, z, vf):  # compute_results (spmv.cpp:66-104): ((0 + t0) + t1) + ... per VF group
+        t = 0.0
+        for k in range(vf):
+            t = t + vals[g + k] * x[cols[g + k]]
+        acc = acc + t
+        if flags[g + vf - 1]:
+            y[r] = acc
+            acc, r = 0.0, r + 1
+    ref = oracle.spmv_fpga_order(rp, col, val, x, 4, 32768, vf)
+    assert np.array_equal(y, ref)
