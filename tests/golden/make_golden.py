@@ -78,6 +78,14 @@ def fixtures():
     out["longrow"] = (n, m, random_rows(rng, n, m, lens))
     # a single row
     out["onerow"] = (1, 700, random_rows(rng, 1, 700, [600]))
+    # the 4x4 example of the reference's diagrams (images/1_matrix.svg), a..h = 1..8
+    # (tests/golden/reference_diagram_kat.json); no random draws, so the fixtures above keep
+    # their bytes
+    with open(os.path.join(OUT, "reference_diagram_kat.json")) as f:
+        ent = json.load(f)["matrix_4x4"]["entries"]
+    rows = [(np.array([c for r, c, _ in ent if r == i]),
+             np.array([float("abcdefgh".index(v) + 1) for r, _, v in ent if r == i])) for i in range(4)]
+    out["diagram"] = (4, 4, rows)
     return out
 
 
