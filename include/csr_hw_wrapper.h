@@ -77,7 +77,8 @@ typedef struct spmv_plan_stats {
     uint64_t device_bytes;       /* bytes of the hw representation resident in HBM */
     uint64_t algorithmic_bytes;  /* compulsory CSR bytes per SpMV, SURVEY.md §8(d) */
     int32_t device;              /* HIP device ordinal */
-    int32_t kernel;              /* 0 = flagged-tile gather, 2 = panel sweep */
+    int32_t kernel;              /* 0 = flagged-tile gather, 1 = spmv_gold order (bitwise), 2 = panel
+                                    sweep */
     int32_t blocks;              /* column blocks of the representation */
     int32_t format;              /* bit 0: 16- or 8-bit column offsets per tile (kernel 0), bit 3:
                                     8-bit; bit 1: packed 12/8-byte sweep entries; bit 2:

@@ -31,7 +31,34 @@ static int requested_kernel()
         return kKernelTiles;
     if (!std::strcmp(e, "sweep"))
         return kKernelSweep;
+    if (!std::strcmp(e, "gold"))
+        return kKernelGold;
     return -1;
+}
+
+// Gold-order representation (kernel 1): the CSR itself plus the list of long rows.
+static int build_gold(spmv_plan &p, const IndexType *h_row_ptr, const IndexType *d_col_src,
+                      const ValueType *d_val_src, hipStream_t s)
+{
+    std::vector<uint32_t> longs;
+    for (IndexType r = 0; r < p.nr_rows; ++r)
+        if (h_row_ptr[r + 1] - h_row_ptr[r] > (IndexType)kGoldLong)
+            longs.push_back(r);
+    p.nlong = longs.size();
+    SPMV_TRY(hipMalloc((void **)&p.d_rp, (size_t(p.nr_rows) + 1) * sizeof(uint32_t)));
+    SPMV_TRY(hipMalloc((void **)&p.d_col, std::max<uint64_t>(p.nnz, 1) * sizeof(uint32_t)));
+    SPMV_TRY(hipMalloc((void **)&p.d_val, std::max<uint64_t>(p.nnz, 1) * sizeof(ValueType)));
+    if (p.nlong)
+        SPMV_TRY(hipMalloc((void **)&p.d_long, p.nlong * sizeof(uint32_t)));
+    SPMV_TRY(hipMemcpyAsync(p.d_rp, h_row_ptr, (size_t(p.nr_rows) + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (p.nnz) {
+        SPMV_TRY(hipMemcpyAsync(p.d_col, d_col_src, p.nnz * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        SPMV_TRY(hipMemcpyAsync(p.d_val, d_val_src, p.nnz * sizeof(ValueType), hipMemcpyDeviceToDevice, s));
+    }
+    if (p.nlong)
+        SPMV_TRY(hipMemcpyAsync(p.d_long, longs.data(), p.nlong * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipStreamSynchronize(s));  // the host vector goes out of scope
+    return 0;
 }
 
 // Flagged-tile representation (kernel 0): row-end bitmap, tile table, packed col/val.
@@ -252,7 +279,10 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             return 1;
         }
     }
-    if (kernel != kKernelSweep) {
+    if (kernel == kKernelGold) {
+        if (build_gold(*p, h_row_ptr, d_col, d_val, s))
+            return 1;
+    } else if (kernel != kKernelSweep) {
         if (build_tiles(*p, h_row_ptr, d_col, d_val, s))
             return 1;
     }
@@ -271,7 +301,7 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_rp, (void *)d_long,
                       (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase})
         if (ptr)
             (void)hipFree(ptr);
@@ -285,6 +315,8 @@ spmv_plan::~spmv_plan()
 
 uint64_t spmv_plan::device_bytes() const
 {
+    if (kernel == kKernelGold)
+        return (uint64_t(nr_rows) + 1) * 4 + nnz * (4 + sizeof(ValueType)) + nlong * 4;
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
@@ -356,7 +388,7 @@ static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStrea
 {
     if (p->nr_rows == 0)
         return 0;
-    if (p->kernel != kKernelSweep && (p->has_empty || p->nnz == 0))
+    if (p->kernel == kKernelTiles && (p->has_empty || p->nnz == 0))
         SPMV_TRY(hipMemsetAsync(d_y, 0, size_t(p->nr_rows) * sizeof(ValueType), s));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {
@@ -372,8 +404,8 @@ static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStrea
         p->ev_used += 2;
         SPMV_TRY(hipEventRecord(e0, s));
     }
-    if (p->kernel == kKernelSweep) {
-        SPMV_TRY(launch_sweep(*p, d_x, d_y, s));
+    if (p->kernel == kKernelSweep || p->kernel == kKernelGold) {
+        SPMV_TRY(p->kernel == kKernelSweep ? launch_sweep(*p, d_x, d_y, s) : launch_gold(*p, d_x, d_y, s));
         if (timing)
             SPMV_TRY(hipEventRecord(e1, s));
         return 0;
@@ -459,8 +491,10 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->nr_cols = p->nr_cols;
     st->nr_nzeros = p->nnz;
     st->nr_nonempty_rows = p->nzr;
-    st->nr_tiles = p->kernel == kKernelSweep ? p->nunits : p->ntiles;
-    st->tile_nnz = p->kernel == kKernelSweep ? (p->nunits ? p->ent_pad / p->nunits : 0) : kTileNnz;
+    // work units of the main kernel: tiles, sweep units (panel pieces), or long rows (gold)
+    st->nr_tiles = p->kernel == kKernelSweep ? p->nunits : p->kernel == kKernelGold ? p->nlong : p->ntiles;
+    st->tile_nnz = p->kernel == kKernelSweep ? (p->nunits ? p->ent_pad / p->nunits : 0)
+                   : p->kernel == kKernelGold ? (uint64_t)kGoldLong : kTileNnz;
     st->device_bytes = p->device_bytes();
     st->algorithmic_bytes = p->algorithmic_bytes();
     st->device = p->device;

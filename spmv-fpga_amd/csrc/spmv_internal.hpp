@@ -43,7 +43,9 @@ constexpr uint64_t kSweepChunk = 128;              // entries per packed chunk (
 
 // plan kernels (spmv_plan_stats.kernel)
 constexpr int kKernelTiles = 0;  // flagged-tile wave kernel, x gathered through the caches
+constexpr int kKernelGold = 1;   // spmv_gold's exact order (bitwise reference results)
 constexpr int kKernelSweep = 2;  // panel sweep: y in LDS, columns swept in order (x from L2)
+constexpr int kGoldLong = 128;   // gold kernel: rows longer than this get a whole wave
 
 }  // namespace spmvhw
 
@@ -70,6 +72,11 @@ struct spmv_plan {
     ValueType *d_tail = nullptr;
     uint32_t *d_cross = nullptr;   // rows crossing tile boundaries: (row, first tile, last tile)
     uint64_t ncross = 0;
+
+    // gold-order representation (kernel 1, gold.hip): plain CSR in d_rp / d_col / d_val
+    uint32_t *d_rp = nullptr;         // rebased row_ptr[nr_rows + 1]
+    uint32_t *d_long = nullptr;       // rows with more than kGoldLong entries
+    uint64_t nlong = 0;
 
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
@@ -124,6 +131,9 @@ hipError_t launch_tile_span(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles
 // col - cbase[tile] as `bytes`-wide offsets (2 or 1)
 hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_cbase,
                          void *d_out, int bytes, hipStream_t s);
+
+// gold.hip
+hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);
 
 // sweep.hip
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);

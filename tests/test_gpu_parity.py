@@ -27,8 +27,8 @@ def torch():
     return t
 
 
-KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked"]
-KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2}
+KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "gold"]
+KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "gold": 1}
 
 
 @pytest.fixture(params=KERNELS)
@@ -204,7 +204,7 @@ def test_deterministic(torch, kernel, dtype):
     lib = spmv_hw.load(dtype)
     y1, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
     y2, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
-    if kernel.startswith("tiles"):
+    if kernel.startswith("tiles") or kernel == "gold":
         assert np.array_equal(y1.view(np.uint8), y2.view(np.uint8))
     else:
         assert oracle.scaled_error(row_ptr, col, val, x, y1, y2) <= TIGHT[np.dtype(dtype)]
@@ -392,6 +392,73 @@ def test_sweep_split_pieces_match_oracle(torch, monkeypatch, dtype):
     ref = oracle.spmv_gold(row_ptr, c, v, xx)
     for split, (_, y) in ys.items():
         check(row_ptr, c, v, xx, ref, y, dtype)
+
+
+# ---- gold order: bitwise the reference's spmv_gold (csr.cpp:184-194) ----
+def _bitwise(a, b):
+    assert a.dtype == b.dtype and a.shape == b.shape
+    bad = np.nonzero(a.view(np.uint8).reshape(len(a), -1).any(axis=1) !=
+                     b.view(np.uint8).reshape(len(b), -1).any(axis=1))[0]
+    assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), f"first differing rows {bad[:5]}"
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("dtype,tag", DTYPES)
+def test_gold_kernel_bitwise_equals_fixture(torch, monkeypatch, name, dtype, tag):
+    monkeypatch.setenv("SPMV_HW_KERNEL", "gold")
+    lib = spmv_hw.load(dtype)
+    path = os.path.join(GOLDEN, manifest()[name]["file"])
+    _, c, row_ptr, col, val, _ = oracle.read_csr(path, dtype)
+    x, y_gold = golden_arrays(name, tag)
+    y, st = run_device(torch, lib, row_ptr, col, val, x, c, expect_kernel="gold")
+    _bitwise(y, y_gold)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("workload", ["powerlaw", "banded"])
+def test_gold_kernel_bitwise_equals_oracle_synthetic(torch, monkeypatch, dtype, workload):
+    """1M rows: power-law rows up to ~20K entries exercise the wave-per-long-row path."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "gold")
+    lib = spmv_hw.load(dtype)
+    n = 1_000_000
+    if workload == "powerlaw":
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 16 * n, seed=4)
+    else:
+        rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    st = plan.stats()
+    assert st["kernel"] == 1 and (st["nr_tiles"] > 0) == (workload == "powerlaw")  # long rows
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    h = [t.cpu().numpy() for t in (rp, col, val, x, y)]
+    row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
+    _bitwise(yy, oracle.spmv_gold(row_ptr, c, v, xx))
+    plan.destroy()
+
+
+@pytest.mark.parametrize("units", [1, 3])
+def test_gold_kernel_through_reference_api_is_bitwise(torch, monkeypatch, units):
+    """main.cpp's flow with SPMV_HW_KERNEL=gold: y_fpga (zeroed, then +=) equals spmv_gold's y
+    bit for bit, so the reference's own verification sees zero difference."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "gold")
+    monkeypatch.setenv("SPMV_NGPUS", str(units))
+    lib = spmv_hw.load(np.float64)
+    for name in FIXTURES:
+        path = os.path.join(GOLDEN, manifest()[name]["file"])
+        n, c, row_ptr, col, val, _ = oracle.read_csr(path, np.float64)
+        x, y_gold = golden_arrays(name, "f64")
+        m = lib.make_csr_matrix(row_ptr, col, val, c)
+        hw, bm = lib.create_csr_hw_matrix(m)
+        hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(x), hw[0].contents.blocks, hw[0].contents.nr_cols)
+        y_vec = lib.make_csr_vector(np.zeros(n))
+        lib.spmv_hw(hw, hx, y_vec, bm)
+        y = np.ctypeslib.as_array(y_vec.values, (n,)).copy()
+        lib.delete_csr_hw_matrix(hw)
+        lib.free_bitmap(bm)
+        lib.delete_csr_hw_x_vector(hx)
+        _bitwise(y, y_gold)
 
 
 def test_auto_kernel_choice(torch, monkeypatch):
