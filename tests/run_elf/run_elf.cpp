@@ -4,7 +4,10 @@
 // oracle here (oracle/csr_ref.c), which is exactly what main.cpp links from csr.cpp; the
 // hardware path is libspmv_hw (include/csr_hw_wrapper.h) with no CPU fallback.
 //
-// Usage: run.elf <matrix-file>     (env SPMV_NGPUS = units, like the reference's CU knob)
+// Usage: run.elf <matrix-file> [--fast-reader]   (env SPMV_NGPUS = units, like the reference's
+// CU knob). --fast-reader reads the file with the library's Part-3 reader (spmv_read_csr_*,
+// the drop-in for csr.cpp's read_csr_header / read_csr_matrix) instead of the oracle's, and
+// prints the file read time.
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
@@ -36,12 +39,15 @@ int main(int argc, char **argv)
 #else
     std::cout << "Welcome to SpMV (Compute Units : " << units << ", MI355X, double-precision arithmetic)\n";
 #endif
-    if (argc != 2) {
+    const bool fast = argc == 3 && std::string(argv[2]) == "--fast-reader";
+    if (argc != 2 && !fast) {
         std::printf("please enter the input file name  \n");
         return 1;
     }
+    const double rd0 = now_us();
     csr_header hdr;
-    if (oracle_read_csr_header(argv[1], &hdr.nr_rows, &hdr.nr_cols, &hdr.nr_nzeros, 32768, &hdr.blocks)) {
+    if (fast ? spmv_read_csr_header(&hdr, argv[1])
+             : oracle_read_csr_header(argv[1], &hdr.nr_rows, &hdr.nr_cols, &hdr.nr_nzeros, 32768, &hdr.blocks)) {
         std::cout << "Error reading matrix header\n";
         return 1;
     }
@@ -53,10 +59,14 @@ int main(int argc, char **argv)
     matrix.col_ind = (IndexType *)std::malloc((hdr.nr_nzeros + 1) * sizeof(IndexType));
     matrix.values = (ValueType *)std::malloc((hdr.nr_nzeros + 1) * sizeof(ValueType));
     matrix.Filename = argv[1];
-    if (oracle_read_csr_matrix(argv[1], hdr.nr_rows, hdr.nr_nzeros, matrix.row_ptr, matrix.col_ind, matrix.values)) {
+    if (fast ? spmv_read_csr_matrix(&matrix, argv[1])
+             : oracle_read_csr_matrix(argv[1], hdr.nr_rows, hdr.nr_nzeros, matrix.row_ptr, matrix.col_ind,
+                                      matrix.values)) {
         std::cout << "Error reading matrix\n";
         return 1;
     }
+    std::printf("File read time          : %.6f ms elapsed (%s reader)\n", (now_us() - rd0) / 1000,
+                fast ? "spmv_read_csr" : "oracle");
     csr_vector x{(ValueType *)std::calloc(hdr.nr_cols + 1, sizeof(ValueType)), hdr.nr_cols};
     oracle_init_vector_rand(x.values, x.nr_values, 1);
     csr_vector y{(ValueType *)std::calloc(hdr.nr_rows + 1, sizeof(ValueType)), hdr.nr_rows};

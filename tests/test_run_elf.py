@@ -11,10 +11,12 @@ pytestmark = pytest.mark.gpu
 ELF = os.path.join(ROOT, "tests", "run_elf")
 
 
-@pytest.mark.parametrize("name", ["small", "small_empty", "trail", "wide", "longrow", "onerow"])
+@pytest.mark.parametrize("name", ["small", "small_empty", "trail", "wide", "longrow", "onerow", "diagram"])
 @pytest.mark.parametrize("units", ["1", "2"])
-def test_run_elf_f64_passes(name, units):
-    out = subprocess.run([os.path.join(ELF, "run.elf"), os.path.join(GOLDEN, f"{name}.mtx")],
+@pytest.mark.parametrize("reader", ["oracle", "fast"])
+def test_run_elf_f64_passes(name, units, reader):
+    extra = ["--fast-reader"] if reader == "fast" else []
+    out = subprocess.run([os.path.join(ELF, "run.elf"), os.path.join(GOLDEN, f"{name}.mtx")] + extra,
                          capture_output=True, text=True, timeout=120, env=dict(os.environ, SPMV_NGPUS=units))
     assert out.returncode == 0, out.stdout + out.stderr
     for line in ("Welcome to SpMV", "Software execution time", "Matrix read time", "Total non-zeros",
