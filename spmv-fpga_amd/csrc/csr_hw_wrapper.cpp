@@ -112,6 +112,11 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         die("create_csr_hw_matrix: null argument");
     const int units = spmv_hw_units();
     const IndexType n = matrix->nr_rows;
+    const bool trace = std::getenv("SPMV_HW_TRACE") != nullptr;
+    const double t0 = timestamp_us();
+    (void)device_count();  // the first HIP call of the process initialises the runtime
+    if (trace)
+        std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "HIP runtime init", (timestamp_us() - t0) / 1000);
     std::vector<IndexType> bounds(units + 1, 0);
     if (spmv_partition_rows(matrix->row_ptr, n, units, bounds.data()))
         die(spmv_hw_last_error());

@@ -9,6 +9,7 @@
 //   create_block_matrix +
 //   generate_balanced_hw_submatrix (:190-318) -> k_pack on the GPU (O(nnz), coalesced)
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -20,6 +21,23 @@ namespace spmvhw {
 static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 const char *get_error() { return g_err.c_str(); }
+
+// env SPMV_HW_TRACE=1: phase times of plan construction on stderr
+struct PhaseTrace {
+    const bool on = std::getenv("SPMV_HW_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+    void operator()(const char *phase, hipStream_t s)
+    {
+        if (!on)
+            return;
+        (void)hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms (total %9.3f ms)\n", phase,
+                     std::chrono::duration<double, std::milli>(now - last).count(),
+                     std::chrono::duration<double, std::milli>(now - t0).count());
+        last = now;
+    }
+};
 
 // Which kernel a plan uses: env SPMV_HW_KERNEL = tiles | sweep | auto (default).
 static int requested_kernel()
@@ -193,6 +211,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
                                  const ValueType *val_src, bool src_on_device, hipStream_t s)
 {
     *out = nullptr;
+    PhaseTrace trace;
     if (nr_rows > 0 && h_row_ptr[0] != 0) {
         set_error("row_ptr must be rebased to 0");
         return 1;
@@ -235,6 +254,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         d_col = (const IndexType *)tcol.p;
         d_val = (const ValueType *)tval.p;
     }
+    trace("row_ptr scan + upload", s);
     if (nnz) {
         SPMV_TRY(hipMalloc(&tbad.p, sizeof(uint32_t)));
         SPMV_TRY(hipMemsetAsync(tbad.p, 0, sizeof(uint32_t), s));
@@ -266,6 +286,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         }
     }
     p->kernel = kernel;
+    trace("validate + kernel choice", s);
     if (const char *t = std::getenv("SPMV_SWEEP_THREADS")) {
         const int v = std::atoi(t);
         if (v == 256 || v == 512 || v == 1024)
@@ -287,6 +308,8 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             return 1;
     }
     SPMV_TRY(hipStreamSynchronize(s));
+    trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelGold ? "build gold layout"
+                                                                                    : "build tile layout", s);
     *out = p.release();
     return 0;
 }
