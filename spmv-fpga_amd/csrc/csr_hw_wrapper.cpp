@@ -223,9 +223,8 @@ void create_csr_hw_x_vector(csr_hw_vector **hw_x, csr_vector *x, int blocks, Ind
         ValueType *p = nullptr;
         check(hipMalloc((void **)&p, std::max<size_t>(cols, 1) * sizeof(ValueType)), "hipMalloc(x)");
         check(hipMemset(p, 0, std::max<size_t>(cols, 1) * sizeof(ValueType)), "hipMemset(x)");
-        if (x->nr_values)
-            check(hipMemcpy(p, x->values, size_t(x->nr_values) * sizeof(ValueType), hipMemcpyHostToDevice),
-                  "hipMemcpy(x)");
+        if (x->nr_values && upload_staged(p, x->values, size_t(x->nr_values) * sizeof(ValueType), nullptr))
+            die(std::string("create_csr_hw_x_vector: ") + spmv_hw_last_error());
         v->per_device[d] = p;
     }
     v->vals[0] = reinterpret_cast<BusDataType *>(v->per_device[0]);

@@ -13,6 +13,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <thread>
 
 #include "spmv_internal.hpp"
 
@@ -21,6 +23,53 @@ namespace spmvhw {
 static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 const char *get_error() { return g_err.c_str(); }
+
+// Host -> device copy of a pageable buffer through two pinned 32 MiB staging buffers (process
+// lifetime): host threads fill one buffer while the DMA engine drains the other. A pageable
+// hipMemcpy runs at ~1 GB/s here; this keeps the PCIe link busy instead.
+int upload_staged(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    constexpr size_t kChunk = 32u << 20;
+    if (bytes < (4u << 20)) {
+        SPMV_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        SPMV_TRY(hipStreamSynchronize(s));
+        return 0;
+    }
+    static std::mutex mu;
+    static void *buf[2] = {nullptr, nullptr};
+    static hipEvent_t done[2] = {nullptr, nullptr};
+    std::lock_guard<std::mutex> lk(mu);
+    for (int i = 0; i < 2; ++i) {
+        if (!buf[i])
+            SPMV_TRY(hipHostMalloc(&buf[i], kChunk, hipHostMallocPortable));
+        if (!done[i])
+            SPMV_TRY(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+    }
+    bool pending[2] = {false, false};
+    const unsigned hc = std::thread::hardware_concurrency();
+    const int T = (int)std::min(4u, hc ? hc : 1u);
+    int i = 0;
+    for (size_t off = 0; off < bytes; off += kChunk, i ^= 1) {
+        const size_t n = std::min(kChunk, bytes - off);
+        if (pending[i])
+            SPMV_TRY(hipEventSynchronize(done[i]));  // the DMA out of this buffer has finished
+        auto part = [&](int t) {
+            const size_t b = n * t / T, e = n * (t + 1) / T;
+            std::memcpy((char *)buf[i] + b, (const char *)src + off + b, e - b);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t)
+            th.emplace_back(part, t);
+        part(0);
+        for (auto &t : th)
+            t.join();
+        SPMV_TRY(hipMemcpyAsync((char *)dst + off, buf[i], n, hipMemcpyHostToDevice, s));
+        SPMV_TRY(hipEventRecord(done[i], s));
+        pending[i] = true;
+    }
+    SPMV_TRY(hipStreamSynchronize(s));
+    return 0;
+}
 
 // env SPMV_HW_TRACE=1: phase times of plan construction on stderr
 struct PhaseTrace {
@@ -249,8 +298,9 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     if (!src_on_device && nnz) {
         SPMV_TRY(hipMalloc(&tcol.p, nnz * sizeof(IndexType)));
         SPMV_TRY(hipMalloc(&tval.p, nnz * sizeof(ValueType)));
-        SPMV_TRY(hipMemcpyAsync(tcol.p, col_src, nnz * sizeof(IndexType), hipMemcpyHostToDevice, s));
-        SPMV_TRY(hipMemcpyAsync(tval.p, val_src, nnz * sizeof(ValueType), hipMemcpyHostToDevice, s));
+        if (upload_staged(tcol.p, col_src, nnz * sizeof(IndexType), s) ||
+            upload_staged(tval.p, val_src, nnz * sizeof(ValueType), s))
+            return 1;
         d_col = (const IndexType *)tcol.p;
         d_val = (const ValueType *)tval.p;
     }

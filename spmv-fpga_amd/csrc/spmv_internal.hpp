@@ -143,6 +143,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
 int probe_locality(const IndexType *d_rp, const IndexType *d_col, IndexType n, hipStream_t s, double *frac);
 
 // plan.cpp helpers shared with the wrapper
+int upload_staged(void *dst, const void *src, size_t bytes, hipStream_t s);  // pageable H2D, synchronous
 int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,
                                  const IndexType *h_row_ptr /* rebased, nr_rows+1 */,
                                  const IndexType *col_src, const ValueType *val_src,
