@@ -78,14 +78,14 @@ __global__ __launch_bounds__(256) void k_spmv_gold_long(const uint32_t *__restri
         y[r] = acc;
 }
 
-hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
 {
     if (p.nr_rows == 0)
         return hipSuccess;
-    hipLaunchKernelGGL((k_spmv_gold_rows<ValueType>), dim3((p.nr_rows + 255) / 256), dim3(256), 0, s, p.d_rp,
+    launch_or_warm(warm, k_spmv_gold_rows<ValueType>, dim3((p.nr_rows + 255) / 256), dim3(256), 0, s, p.d_rp,
                        p.d_col, p.d_val, d_x, d_y, p.nr_rows);
     if (p.nlong)
-        hipLaunchKernelGGL((k_spmv_gold_long<ValueType>), dim3((unsigned)((p.nlong + 3) / 4)), dim3(256), 0, s,
+        launch_or_warm(warm, k_spmv_gold_long<ValueType>, dim3((unsigned)((p.nlong + 3) / 4)), dim3(256), 0, s,
                            p.d_rp, p.d_col, p.d_val, d_x, p.d_long, (uint32_t)p.nlong, d_y);
     return hipGetLastError();
 }

@@ -240,14 +240,14 @@ __global__ void k_pack(const IndexType *__restrict__ col_src, const V *__restric
     val[dst] = in ? val_src[k] : V(0);
 }
 
-hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
 {
     if (p.ntiles == 0)
         return hipSuccess;
     const uint64_t waves_per_block = kBlockThreads / kWave;
     const uint64_t blocks = (p.ntiles + waves_per_block - 1) / waves_per_block;
 #define SPMV_LAUNCH(VAR, CB)                                                                      \
-    hipLaunchKernelGGL((k_spmv_tiles<ValueType, kTileSteps, VAR, CB>), dim3((unsigned)blocks),     \
+    launch_or_warm(warm, k_spmv_tiles<ValueType, kTileSteps, VAR, CB>, dim3((unsigned)blocks),       \
                        dim3(kBlockThreads), 0, s, p.d_col, p.d_colnar, p.d_tile_cbase, p.d_val,     \
                        p.d_rowend, p.d_tile_info, p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.nnz, \
                        p.ntiles)
@@ -270,12 +270,12 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
     return hipGetLastError();
 }
 
-hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s)
+hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s, bool warm)
 {
     if (p.ncross == 0)
         return hipSuccess;
     const uint64_t blocks = (p.ncross + 255) / 256;
-    hipLaunchKernelGGL((k_fixup<ValueType>), dim3((unsigned)blocks), dim3(256), 0, s, p.d_cross, p.ncross,
+    launch_or_warm(warm, k_fixup<ValueType>, dim3((unsigned)blocks), dim3(256), 0, s, p.d_cross, p.ncross,
                        p.d_head, p.d_tail, p.d_row_id, d_y);
     return hipGetLastError();
 }

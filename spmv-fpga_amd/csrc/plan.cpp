@@ -360,6 +360,18 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     SPMV_TRY(hipStreamSynchronize(s));
     trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelGold ? "build gold layout"
                                                                                     : "build tile layout", s);
+    // load the code objects of the kernels this plan launches (no launch; best effort: a
+    // failure here only means the first run loads them)
+    if (p->kernel == kKernelSweep) {
+        (void)launch_sweep(*p, nullptr, nullptr, s, true);
+    } else if (p->kernel == kKernelGold) {
+        (void)launch_gold(*p, nullptr, nullptr, s, true);
+    } else {
+        (void)launch_spmv(*p, nullptr, nullptr, s, true);
+        (void)launch_fixup(*p, nullptr, s, true);
+    }
+    (void)hipGetLastError();
+    trace("load kernels", s);
     *out = p.release();
     return 0;
 }

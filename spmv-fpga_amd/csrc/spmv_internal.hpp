@@ -117,9 +117,22 @@ namespace spmvhw {
 void set_error(const std::string &msg);
 const char *get_error();
 
+// Launch, or (warm) only have the runtime load the kernel's code object: plan creation runs the
+// launchers warm so that the first SpMV of a plan does not pay the lazy module load (~8 ms).
+template <typename K, typename... Args>
+inline void launch_or_warm(bool warm, K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args)
+{
+    if (warm) {
+        hipFuncAttributes a;
+        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(kernel));
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+    }
+}
+
 // kernels.hip
-hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);
-hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s);
+hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
+hipError_t launch_fixup(const spmv_plan &p, ValueType *d_y, hipStream_t s, bool warm = false);
 hipError_t launch_pack(const IndexType *d_col_src, const ValueType *d_val_src, uint64_t nnz,
                        uint64_t nnz_pad, uint32_t ncols, uint32_t *d_col, ValueType *d_val,
                        uint32_t *d_bad, hipStream_t s);
@@ -133,10 +146,10 @@ hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, 
                          void *d_out, int bytes, hipStream_t s);
 
 // gold.hip
-hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);
+hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
 
 // sweep.hip
-hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s);
+hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
 // 0 ok, 1 error, 2 the padded layout would overflow 32-bit entry offsets (caller may use tiles)
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s);

@@ -401,18 +401,18 @@ __global__ void k_locality(const IndexType *__restrict__ rp, const IndexType *__
 }
 
 template <int T>
-static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
 {
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(SweepAcc);
     const dim3 grid((unsigned)p.nunits), block(T);
     // Unpacked (14-B entries, used when a chunk spans >= 65536 columns): E entries per thread,
     // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
-    hipLaunchKernelGGL((k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>), grid, block, lds, s, p.d_s_col, \
+    launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>, grid, block, lds, s, p.d_s_col,   \
                        p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, p.d_part, p.panel_rmax + 1, d_x, d_y)
     if (p.sweep_packed) {
 #define PK(Q, LAG)                                                                                  \
-    hipLaunchKernelGGL((k_spmv_sweep_packed<ValueType, T, Q, true, LAG>), grid, block, lds, s, p.d_s_col, \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, true, LAG>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, p.d_part, p.panel_rmax + 1, d_x, d_y)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
@@ -444,18 +444,18 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #undef SWEEP
 }
 
-hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s)
+hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
 {
     if (p.npanels == 0)
         return hipSuccess;
     switch (p.sweep_threads) {
-    case 256: launch_sweep_t<256>(p, d_x, d_y, s); break;
-    case 512: launch_sweep_t<512>(p, d_x, d_y, s); break;
-    default: launch_sweep_t<1024>(p, d_x, d_y, s); break;
+    case 256: launch_sweep_t<256>(p, d_x, d_y, s, warm); break;
+    case 512: launch_sweep_t<512>(p, d_x, d_y, s, warm); break;
+    default: launch_sweep_t<1024>(p, d_x, d_y, s, warm); break;
     }
     if (p.sweep_split > 1) {
         const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
-        hipLaunchKernelGGL((k_sweep_combine<ValueType>), grid, dim3(256), 0, s, p.d_panel_row, p.sweep_split,
+        launch_or_warm(warm, k_sweep_combine<ValueType>, grid, dim3(256), 0, s, p.d_panel_row, p.sweep_split,
                            p.d_part, p.panel_rmax + 1, d_y);
     }
     return hipGetLastError();
