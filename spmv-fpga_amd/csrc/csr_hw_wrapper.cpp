@@ -131,6 +131,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         h->row_end = bounds[u + 1];
         if (spmv_plan_create_host(&h->plan, h->device, matrix, h->row_begin, h->row_end))
             die(std::string("create_csr_hw_matrix: ") + spmv_hw_last_error());
+        (void)unit_stream(u);  // created here, not inside spmv_hw's timed region
         spmv_plan_stats st;
         spmv_plan_get_stats(h->plan, &st);
         const spmv_plan &pl = *h->plan;
@@ -258,6 +259,11 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         }
     }
 
+    const bool trace = std::getenv("SPMV_HW_TRACE") != nullptr;
+    auto tr = [&](const char *what, double since) {
+        if (trace)
+            std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", what, (timestamp_us() - since) / 1000);
+    };
     // kernels of every unit (one stream per unit; units on different GPUs run concurrently)
     const double hw_s = timestamp_us();
     for (int u = 0; u < units; ++u) {
@@ -267,6 +273,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         if (spmv_plan_run(m->plan, x->per_device[m->device], m->d_y, unit_stream(u)))
             die(std::string("spmv_hw: ") + spmv_hw_last_error());
     }
+    tr("spmv_hw: launches", hw_s);
     for (int u = 0; u < units; ++u) {
         check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
         check(hipStreamSynchronize(unit_stream(u)), "spmv kernels");
@@ -287,6 +294,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
                              unit_stream(u)),
               "hipMemcpyAsync(y)");
     }
+    tr("spmv_hw: D2H enqueue", ra_s);
     const unsigned hc = std::thread::hardware_concurrency();
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
@@ -295,6 +303,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
             continue;
         check(hipSetDevice(m->device), "hipSetDevice");
         check(hipStreamSynchronize(unit_stream(u)), "y copy");
+        tr("spmv_hw: D2H done", ra_s);
         ValueType *dst = y_fpga->values + m->row_begin;
         const ValueType *src = m->h_stage;
         const int T = rows < (1u << 20) ? 1 : (int)std::min(8u, hc ? hc : 1u);
@@ -313,6 +322,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
                 t.join();
         }
     }
+    tr("spmv_hw: host accumulation", ra_s);
     const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
     std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
     std::printf("Total time  : %.6f ms elapsed\n", hw_exec + ra_exec);
