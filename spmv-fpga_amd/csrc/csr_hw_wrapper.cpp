@@ -140,7 +140,9 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
             check(hipMalloc((void **)&h->d_y, size_t(rows) * sizeof(ValueType)), "hipMalloc(y)");
             check(hipHostMalloc((void **)&h->h_stage, size_t(rows) * sizeof(ValueType), hipHostMallocDefault),
                   "hipHostMalloc(y stage)");
-            check(hipMemcpyAsync(h->h_stage, h->d_y, sizeof(ValueType), hipMemcpyDeviceToHost, us), "warm D2H");
+            // full size: large copies take a different path whose first use costs ~20 ms
+            check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
+                  "warm D2H");
             check(hipStreamSynchronize(us), "warm D2H");
         }
         spmv_plan_stats st;
