@@ -31,6 +31,7 @@ for s in $STEPS; do
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
     calib) run calib 300 tools/hbm_calib ;;
     strong) run strong 600 python tools/strong_slices.py ${STRONG_ARGS:-} ;;
+    skew) run skew 600 python tools/skew_probe.py ${SKEW_ARGS:-} ;;
     e2e) run reader 600 python tools/bench_reader.py --dir /tmp --threads 1,8,16
          run run_elf_16m 600 ./tests/run_elf/run.elf /tmp/reader_1000000_16000000.mtx --fast-reader ;;
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
