@@ -386,7 +386,7 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_rp, (void *)d_long,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp, (void *)d_long,
                       (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase})
         if (ptr)
             (void)hipFree(ptr);
@@ -405,7 +405,7 @@ uint64_t spmv_plan::device_bytes() const
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
-               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * 8 : 0);
+               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * 8 : 0) + nunits * 4 + (npanels + 1) * 4;
     return nnz_pad * (tile_col_bytes + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
            (tile_col_bytes < 4 ? ntiles * 4 : 0) +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;

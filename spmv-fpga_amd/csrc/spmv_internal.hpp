@@ -81,7 +81,9 @@ struct spmv_plan {
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
     uint64_t nunits = 0;               // workgroups of a launch = npanels * sweep_split
-    uint32_t sweep_split = 1;          // pieces per panel (column ranges); > 1: partials + combine
+    uint32_t sweep_split = 1;          // > 1: some panel is cut into pieces (partials + combine)
+    uint32_t *d_unit_panel = nullptr;  // panel of each work unit
+    uint32_t *d_panel_unit = nullptr;  // first unit of each panel [npanels + 1]
     double *d_part = nullptr;          // split > 1: nunits x (panel_rmax + 1) fp64 partial sums
     uint32_t panel_rmax = 0;
     int sweep_threads = spmvhw::kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)

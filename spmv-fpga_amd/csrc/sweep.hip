@@ -18,8 +18,9 @@
 //   s_row u16[ent_pad]  row inside the panel (padding entries use the scratch slot R_p)
 //   s_val V[ent_pad]    value
 //   panel_row u32[P+1]  row range of panel p
-//   unit_ent u32[U+1]   entry range of work unit u = (panel u / split, piece u % split); with
-//                       split = 1 the panel's whole (128-padded) entry range
+//   unit_ent u32[U+1]   entry range of work unit u (a piece of whole chunks of one panel; a
+//                       panel's pieces are consecutive units); one piece = the whole panel
+//   unit_panel u32[U]   panel of unit u;  panel_unit u32[P+1]  first unit of each panel
 // Packed form (default when every 128-entry chunk spans < 65536 columns, 12 B/entry):
 //   s_col u32 holds (row_in_panel << 16) | (column - s_cbase[chunk]); s_row is dropped; inside a
 //   chunk, word 2l+j holds entry 64j+l (k_sweep_lane_order) so one gather instruction covers 64
@@ -94,14 +95,14 @@ __device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o
     }
 }
 
-// A unit's y: stored when the panel is one unit; with split pieces (split > 1) each piece
-// stores its fp64 partial sums (its column range) into part[unit * stride + i], and
-// k_sweep_combine adds the pieces of every row in piece order (deterministic, one rounding).
+// A unit's y: stored when the panel is one unit; a panel cut into pieces has each piece store
+// its fp64 partial sums (its column range) into part[unit * stride + i], and k_sweep_combine
+// adds the pieces of every row in piece order (deterministic, one rounding).
 template <typename V, int T>
 __device__ __forceinline__ void write_panel(const SweepAcc *__restrict__ ylds, uint32_t R, V *__restrict__ y,
-                                            uint32_t split, SweepAcc *__restrict__ part, uint32_t stride)
+                                            uint32_t pieces, SweepAcc *__restrict__ part, uint32_t stride)
 {
-    if (split == 1) {
+    if (pieces == 1) {
         for (uint32_t i = threadIdx.x; i < R; i += T)
             y[i] = V(ylds[i]);
     } else {
@@ -111,20 +112,23 @@ __device__ __forceinline__ void write_panel(const SweepAcc *__restrict__ ylds, u
     }
 }
 
-// y[r0 + i] = sum over the panel's pieces s (in order) of part[(p * split + s) * stride + i]
+// y[r0 + i] = sum over the panel's pieces u (in order) of part[u * stride + i]; panels of one
+// piece were written by the sweep itself
 template <typename V>
-__global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restrict__ panel_row, uint32_t split,
+__global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restrict__ panel_row,
+                                                       const uint32_t *__restrict__ panel_unit,
                                                        const SweepAcc *__restrict__ part, uint32_t stride,
                                                        V *__restrict__ y)
 {
     const uint32_t p = blockIdx.y;
+    const uint32_t u0 = panel_unit[p], u1 = panel_unit[p + 1];
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= R)
+    if (u1 - u0 < 2 || i >= R)
         return;
-    const SweepAcc *src = part + (uint64_t)p * split * stride + i;
+    const SweepAcc *src = part + (uint64_t)u0 * stride + i;
     SweepAcc acc = src[0];
-    for (uint32_t t = 1; t < split; ++t)
+    for (uint32_t t = 1; t < u1 - u0; ++t)
         acc += src[(uint64_t)t * stride];
     y[r0 + i] = V(acc);
 }
@@ -135,14 +139,16 @@ __global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restric
 template <typename V, int T, int E, int Q, bool SYNC, bool NT>
 __global__ __launch_bounds__(T) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
-    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent, uint32_t split,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
+    const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
     SweepAcc *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef typename EntryVec<E>::C CV;
     typedef typename EntryVec<E>::R RV;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
-    const uint32_t p = blockIdx.x / split;  // unit = (panel, piece of its column-sorted entries)
+    const uint32_t p = unit_panel[blockIdx.x];  // unit = a piece of a panel's column-sorted entries
+    const uint32_t pieces = panel_unit[p + 1] - panel_unit[p];
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     for (uint32_t i = threadIdx.x; i <= R; i += T)
@@ -181,7 +187,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
             __syncthreads();
     }
     __syncthreads();
-    write_panel<V, T>(ylds, R, y + r0, split, part, stride);
+    write_panel<V, T>(ylds, R, y + r0, pieces, part, stride);
 }
 
 // Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
@@ -193,13 +199,15 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
 template <typename V, int T, int Q, bool NT, int LAG = 0>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
-    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent, uint32_t split,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
+    const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
     SweepAcc *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
-    const uint32_t p = blockIdx.x / split;  // unit = (panel, piece of its column-sorted entries)
+    const uint32_t p = unit_panel[blockIdx.x];  // unit = a piece of a panel's column-sorted entries
+    const uint32_t pieces = panel_unit[p + 1] - panel_unit[p];
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     __shared__ uint32_t progress[T / 64];
@@ -265,7 +273,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         }
     }
     __syncthreads();
-    write_panel<V, T>(ylds, R, y + r0, split, part, stride);
+    write_panel<V, T>(ylds, R, y + r0, pieces, part, stride);
 }
 
 // chunk c of 128 entries: base = min column; fails the plan's packing when the span >= 65536
@@ -411,11 +419,11 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>, grid, block, lds, s, p.d_s_col,   \
-                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, p.d_part, p.panel_rmax + 1, d_x, d_y)
+                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
     if (p.sweep_packed) {
 #define PK(Q, LAG)                                                                                  \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, true, LAG>, grid, block, lds, s, p.d_s_col, \
-                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.sweep_split, p.d_part, p.panel_rmax + 1, d_x, d_y)
+                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
         case 15: PK(2, 0); break;
@@ -457,7 +465,7 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
     }
     if (p.sweep_split > 1) {
         const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
-        launch_or_warm(warm, k_sweep_combine<ValueType>, grid, dim3(256), 0, s, p.d_panel_row, p.sweep_split,
+        launch_or_warm(warm, k_sweep_combine<ValueType>, grid, dim3(256), 0, s, p.d_panel_row, p.d_panel_unit,
                            p.d_part, p.panel_rmax + 1, d_y);
     }
     return hipGetLastError();
@@ -545,19 +553,40 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     p.npanels = P;
     p.panel_rmax = rmax_used;
     p.ent_pad = poff[P];
-    // work units: `split` pieces of whole chunks per panel
+    // work units: pieces of whole chunks per panel. split mode: `split` pieces each; any panel
+    // with more than twice the mean entry count (a panel holding very long rows) is cut
+    // further, so that no workgroup gets more than ~2x the mean work
     const uint32_t split = split_mode ? std::max<uint32_t>(1, (uint32_t)cus / P) : 1;
-    std::vector<uint32_t> uent((size_t)P * split + 1);
+    const double mean = P ? double(padded) / P : 0.0;
+    std::vector<uint32_t> punit(P + 1, 0);
     for (uint32_t q = 0; q < P; ++q) {
         const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
-        for (uint32_t t = 0; t < split; ++t)
-            uent[(size_t)q * split + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / split));
+        uint64_t k = split * std::max<uint64_t>(
+                                 1, (uint64_t)std::ceil(double(poff[q + 1] - poff[q]) / std::max(2.0 * mean, 1.0)));
+        k = std::max<uint64_t>(1, std::min<uint64_t>(k, chunks));
+        punit[q + 1] = punit[q] + (uint32_t)k;
     }
-    uent[(size_t)P * split] = poff[P];
-    p.sweep_split = split;
-    p.nunits = (uint64_t)P * split;
-    if (split > 1)
-        SPMV_TRY(hipMalloc((void **)&p.d_part, p.nunits * (uint64_t(rmax_used) + 1) * sizeof(SweepAcc)));
+    const uint32_t U = punit[P];
+    std::vector<uint32_t> uent((size_t)U + 1), upanel(std::max<uint32_t>(U, 1));
+    bool multi = false;
+    for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
+        const uint32_t k = punit[q + 1] - punit[q];
+        multi |= k > 1;
+        for (uint32_t t = 0; t < k; ++t) {
+            uent[punit[q] + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / k));
+            upanel[punit[q] + t] = q;
+        }
+    }
+    uent[U] = poff[P];
+    p.sweep_split = multi ? std::max<uint32_t>(split, 2) : 1;  // > 1: combine kernel needed
+    p.nunits = U;
+    if (multi)
+        SPMV_TRY(hipMalloc((void **)&p.d_part, (uint64_t)U * (uint64_t(rmax_used) + 1) * sizeof(SweepAcc)));
+    SPMV_TRY(hipMalloc((void **)&p.d_unit_panel, upanel.size() * 4));
+    SPMV_TRY(hipMalloc((void **)&p.d_panel_unit, punit.size() * 4));
+    SPMV_TRY(hipMemcpyAsync(p.d_unit_panel, upanel.data(), upanel.size() * 4, hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipMemcpyAsync(p.d_panel_unit, punit.data(), punit.size() * 4, hipMemcpyHostToDevice, s));
 
     // bucket shift so that P * buckets fits 32-bit keys
     uint32_t shift = 0;

@@ -461,6 +461,27 @@ def test_gold_kernel_through_reference_api_is_bitwise(torch, monkeypatch, units)
         _bitwise(y, y_gold)
 
 
+@pytest.mark.parametrize("kern", ["sweep", "tiles", "gold"])
+def test_dense_rows_among_short_ones(torch, monkeypatch, kern):
+    """Ragged extreme: two rows of 600K entries among 400K rows of ~16. The sweep cuts the
+    panels holding them into pieces (more units than panels); the tiles carry them across
+    ~1200 tiles each through the fix-up; gold gives them a wave each."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", kern)
+    rng = np.random.default_rng(12)
+    n, m = 400_000, 1_000_000
+    lens = rng.poisson(16, n)
+    dense = [77, 250_001]
+    lens[dense] = 600_000
+    row_ptr, col, val, x = random_csr(rng, n, m, lens, np.float64)
+    lib = spmv_hw.load(np.float64)
+    y, st = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel=kern)
+    ref = oracle.spmv_gold(row_ptr, col, val, x)
+    if kern == "gold":
+        assert np.array_equal(y.view(np.uint8), ref.view(np.uint8))
+    else:
+        check(row_ptr, col, val, x, ref, y, np.float64)
+
+
 def test_auto_kernel_choice(torch, monkeypatch):
     """Automatic choice: banded (local columns) -> tiles; power-law with columns spread over an x
     much larger than the L2s -> sweep."""
