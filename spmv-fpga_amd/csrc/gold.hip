@@ -71,8 +71,16 @@ __global__ __launch_bounds__(256) void k_spmv_gold_long(const uint32_t *__restri
         if (k < e)
             prod = val[k] * x[col[k]];
         const int cnt = (int)min((uint32_t)kWave, e - base);
-        for (int t = 0; t < cnt; ++t)
-            acc = acc + read_lane(prod, t);  // wave-uniform: every lane holds the same acc
+        if (cnt == kWave) {
+            // constant lanes: the readlanes do not depend on acc and issue ahead of the add
+            // chain, which then costs one dependent v_add per entry
+#pragma unroll
+            for (int t = 0; t < kWave; ++t)
+                acc = acc + read_lane(prod, t);
+        } else {
+            for (int t = 0; t < cnt; ++t)
+                acc = acc + read_lane(prod, t);  // wave-uniform: every lane holds the same acc
+        }
     }
     if (lane == 0)
         y[r] = acc;
