@@ -259,6 +259,7 @@ def main():
     else:
         kname = "k_spmv_tiles"
     traffic = None
+    l2_requests = None  # TCC_HIT_sum + TCC_MISS_sum per launch, same PMC passes
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
@@ -269,19 +270,34 @@ def main():
                          or tr[key]["kernel"].endswith(
                              ", %d>" % (1 if st["format"] & 8 else 2 if st["format"] & 1 else 4)))):
                 traffic = tr[key]["hbm_bytes_per_launch"]
+                cnt = next(iter(tr[key].get("counters", {}).values()), {})
+                if "TCC_HIT_sum" in cnt and "TCC_MISS_sum" in cnt:
+                    l2_requests = cnt["TCC_HIT_sum"] + cnt["TCC_MISS_sum"]
         except Exception:
             traffic = None
 
     # the achievable HBM read rate measured on MI355X by tools/hbm_calib (dwordx4 stream read,
     # SURVEY §8d "report both"); the roofline fraction stays against the 8 TB/s spec
-    stream_peak = None
+    # and the L2 request ceiling measured by the same tool (L2-resident random gathers): the bound
+    # of the sweep kernel, whose x gathers hit L2
+    stream_peak, l2_peak = None, None
     try:
         for line in open(os.path.join(ROOT, "profiles", "r01_hbm_calib.jsonl")):
             rec = json.loads(line)
             if rec.get("test") == "stream_read":
                 stream_peak = rec["GBps"]
+            if str(rec.get("test", "")).startswith("gather_table_") and rec["test"].endswith("KB") \
+                    and int(rec["test"][13:-2]) <= 4096:
+                l2_peak = max(l2_peak or 0.0, rec["Greq_per_s"])
     except (OSError, ValueError):
-        stream_peak = None
+        stream_peak, l2_peak = None, None
+    l2 = None
+    if l2_requests and kernel_ms > 0:
+        rate = l2_requests / (kernel_ms * 1e-3) / 1e9
+        l2 = {"requests_per_launch": int(l2_requests), "achieved_G_per_s": round(rate, 1),
+              "peak_G_per_s": l2_peak, "frac": round(rate / l2_peak, 4) if l2_peak else None,
+              "src": "TCC_HIT_sum+TCC_MISS_sum (profiles/traffic.json) / kernel_ms; peak = "
+                     "L2-resident gather rate (profiles/r01_hbm_calib.jsonl)"}
 
     exchange = None
     if world > 1:
@@ -340,7 +356,7 @@ def main():
                          "peak_measured": stream_peak,
                          "frac_of_measured": round(achieved / stream_peak, 4) if stream_peak else None,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": kname, "kernel_ms": round(kernel_ms, 5),
+                         "kernel": kname, "kernel_ms": round(kernel_ms, 5), "l2": l2,
                          "kernel_launches": launches, "alg_bytes_per_launch": alg_local},
             "cpu_baseline": cpu,
             "parity": parity,
