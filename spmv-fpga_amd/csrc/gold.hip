@@ -6,83 +6,57 @@
 // scans, LDS atomics) and agree only to rounding; this kernel keeps the exact order, for
 // callers that need results reproducible against the reference bit for bit
 // (env SPMV_HW_KERNEL=gold).
-//   * rows of <= kGoldLong entries: one lane per row walks its entries in order;
-//   * longer rows: one wave per row; the 64 lanes load and multiply 64 consecutive entries at
-//     once, then the products are added into the row's accumulator strictly in order
-//     (v_readlane chain), so the long rows cost one dependent add per entry, not one
-//     dependent load.
-// Multiplies and adds are kept separate (fp contract off). Roofline: the x gathers of an
-// unstructured matrix miss L2 (~55 G/s); this is a correctness mode, not the
-// fast path.
+// One wave per 64 consecutive rows (lane = row). The wave walks its rows' entry range in
+// chunks of kGoldChunk: all 64 lanes load col/val and gather x for the chunk (coalesced,
+// many gathers in flight) and store the products in LDS; then every lane adds its own row's
+// products of the chunk in order. Multiplies and adds are kept separate (fp contract off), so
+// every product and every partial sum is the one spmv_gold computes. Roofline: the x gathers
+// of an unstructured matrix miss L2 (~55 G/s); a correctness mode, not the fast
+// path.
 #include "spmv_internal.hpp"
 
 namespace spmvhw {
 
-template <typename V>
-__device__ __forceinline__ V read_lane(V v, int lane)
+constexpr int kGoldChunk = 1024;  // entries per wave per chunk (8 KiB of fp64 products in LDS)
+
+// the wave's LDS writes complete before any lane reads them (and reads before the next writes)
+__device__ __forceinline__ void wave_lds_sync()
 {
-    if constexpr (sizeof(V) == 8) {
-        const uint64_t u = __builtin_bit_cast(uint64_t, v);
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, lane);
-        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), lane);
-        return __builtin_bit_cast(V, (uint64_t(hi) << 32) | lo);
-    } else {
-        return __builtin_bit_cast(V, __builtin_amdgcn_readlane(__builtin_bit_cast(uint32_t, v), lane));
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <typename V>
-__global__ __launch_bounds__(256) void k_spmv_gold_rows(const uint32_t *__restrict__ rp, const uint32_t *__restrict__ col,
-                                                        const V *__restrict__ val, const V *__restrict__ x,
-                                                        V *__restrict__ y, uint32_t nrows)
+__global__ __launch_bounds__(256) void k_spmv_gold(const uint32_t *__restrict__ rp, const uint32_t *__restrict__ col,
+                                                   const V *__restrict__ val, const V *__restrict__ x,
+                                                   V *__restrict__ y, uint32_t nrows)
 {
 #pragma clang fp contract(off)
-    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= nrows)
-        return;
-    const uint32_t b = rp[r], e = rp[r + 1];
-    if (e - b > (uint32_t)kGoldLong)
-        return;  // k_spmv_gold_long
-    V acc = V(0);
-    for (uint32_t j = b; j < e; ++j) {
-        const V prod = val[j] * x[col[j]];
-        acc = acc + prod;
-    }
-    y[r] = acc;
-}
-
-template <typename V>
-__global__ __launch_bounds__(256) void k_spmv_gold_long(const uint32_t *__restrict__ rp, const uint32_t *__restrict__ col,
-                                                        const V *__restrict__ val, const V *__restrict__ x,
-                                                        const uint32_t *__restrict__ long_rows, uint32_t nlong,
-                                                        V *__restrict__ y)
-{
-#pragma clang fp contract(off)
-    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (w >= nlong)
+    __shared__ V prod[4][kGoldChunk];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t r0 = (blockIdx.x * 4 + w) * kWave;
+    if (r0 >= nrows)
         return;  // wave-uniform
-    const uint32_t r = long_rows[w];
-    const uint32_t b = rp[r], e = rp[r + 1];
+    const uint32_t r = r0 + lane;
+    const bool valid = r < nrows;
+    const uint32_t rb = valid ? rp[r] : 0u, re = valid ? rp[r + 1] : 0u;
+    const uint32_t B = rp[r0], E = rp[min(r0 + (uint32_t)kWave, nrows)];
     V acc = V(0);
-    for (uint32_t base = b; base < e; base += kWave) {
-        const uint32_t k = base + lane;
-        V prod = V(0);
-        if (k < e)
-            prod = val[k] * x[col[k]];
-        const int cnt = (int)min((uint32_t)kWave, e - base);
-        if (cnt == kWave) {
-            // constant lanes: the readlanes do not depend on acc and issue ahead of the add
-            // chain, which then costs one dependent v_add per entry
-#pragma unroll
-            for (int t = 0; t < kWave; ++t)
-                acc = acc + read_lane(prod, t);
-        } else {
-            for (int t = 0; t < cnt; ++t)
-                acc = acc + read_lane(prod, t);  // wave-uniform: every lane holds the same acc
+    for (uint32_t cs = B; cs < E; cs += kGoldChunk) {
+        const uint32_t ce = min(cs + (uint32_t)kGoldChunk, E);
+        for (uint32_t k = cs + lane; k < ce; k += kWave) {
+            const V prd = val[k] * x[col[k]];
+            prod[w][k - cs] = prd;
         }
+        wave_lds_sync();
+        const uint32_t a = max(rb, cs), b = min(re, ce);
+        for (uint32_t k = a; k < b; ++k)
+            acc = acc + prod[w][k - cs];
+        wave_lds_sync();
     }
-    if (lane == 0)
+    if (valid)
         y[r] = acc;
 }
 
@@ -90,11 +64,9 @@ hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
 {
     if (p.nr_rows == 0)
         return hipSuccess;
-    launch_or_warm(warm, k_spmv_gold_rows<ValueType>, dim3((p.nr_rows + 255) / 256), dim3(256), 0, s, p.d_rp,
-                       p.d_col, p.d_val, d_x, d_y, p.nr_rows);
-    if (p.nlong)
-        launch_or_warm(warm, k_spmv_gold_long<ValueType>, dim3((unsigned)((p.nlong + 3) / 4)), dim3(256), 0, s,
-                           p.d_rp, p.d_col, p.d_val, d_x, p.d_long, (uint32_t)p.nlong, d_y);
+    const uint32_t waves = (p.nr_rows + kWave - 1) / kWave;
+    launch_or_warm(warm, k_spmv_gold<ValueType>, dim3((waves + 3) / 4), dim3(256), 0, s, p.d_rp, p.d_col, p.d_val,
+                   d_x, d_y, p.nr_rows);
     return hipGetLastError();
 }
 

@@ -103,28 +103,23 @@ static int requested_kernel()
     return -1;
 }
 
-// Gold-order representation (kernel 1): the CSR itself plus the list of long rows.
+// Gold-order representation (kernel 1): the CSR itself (nlong counts the rows longer than
+// kGoldLong, for the stats only).
 static int build_gold(spmv_plan &p, const IndexType *h_row_ptr, const IndexType *d_col_src,
                       const ValueType *d_val_src, hipStream_t s)
 {
-    std::vector<uint32_t> longs;
+    p.nlong = 0;
     for (IndexType r = 0; r < p.nr_rows; ++r)
-        if (h_row_ptr[r + 1] - h_row_ptr[r] > (IndexType)kGoldLong)
-            longs.push_back(r);
-    p.nlong = longs.size();
+        p.nlong += h_row_ptr[r + 1] - h_row_ptr[r] > (IndexType)kGoldLong;
     SPMV_TRY(hipMalloc((void **)&p.d_rp, (size_t(p.nr_rows) + 1) * sizeof(uint32_t)));
     SPMV_TRY(hipMalloc((void **)&p.d_col, std::max<uint64_t>(p.nnz, 1) * sizeof(uint32_t)));
     SPMV_TRY(hipMalloc((void **)&p.d_val, std::max<uint64_t>(p.nnz, 1) * sizeof(ValueType)));
-    if (p.nlong)
-        SPMV_TRY(hipMalloc((void **)&p.d_long, p.nlong * sizeof(uint32_t)));
     SPMV_TRY(hipMemcpyAsync(p.d_rp, h_row_ptr, (size_t(p.nr_rows) + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     if (p.nnz) {
         SPMV_TRY(hipMemcpyAsync(p.d_col, d_col_src, p.nnz * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         SPMV_TRY(hipMemcpyAsync(p.d_val, d_val_src, p.nnz * sizeof(ValueType), hipMemcpyDeviceToDevice, s));
     }
-    if (p.nlong)
-        SPMV_TRY(hipMemcpyAsync(p.d_long, longs.data(), p.nlong * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    SPMV_TRY(hipStreamSynchronize(s));  // the host vector goes out of scope
+    SPMV_TRY(hipStreamSynchronize(s));
     return 0;
 }
 
@@ -386,7 +381,7 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp, (void *)d_long,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase})
         if (ptr)
             (void)hipFree(ptr);
@@ -401,7 +396,7 @@ spmv_plan::~spmv_plan()
 uint64_t spmv_plan::device_bytes() const
 {
     if (kernel == kKernelGold)
-        return (uint64_t(nr_rows) + 1) * 4 + nnz * (4 + sizeof(ValueType)) + nlong * 4;
+        return (uint64_t(nr_rows) + 1) * 4 + nnz * (4 + sizeof(ValueType));
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
