@@ -52,7 +52,17 @@ __global__ __launch_bounds__(256) void k_spmv_gold(const uint32_t *__restrict__ 
         }
         wave_lds_sync();
         const uint32_t a = max(rb, cs), b = min(re, ce);
-        for (uint32_t k = a; k < b; ++k)
+        uint32_t k = a;
+        for (; k + 16 <= b; k += 16) {  // 16 LDS reads in flight, then the in-order adds
+            V t[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                t[i] = prod[w][k + i - cs];
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                acc = acc + t[i];
+        }
+        for (; k < b; ++k)
             acc = acc + prod[w][k - cs];
         wave_lds_sync();
     }
