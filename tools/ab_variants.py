@@ -16,6 +16,29 @@ import torch  # noqa: E402
 import spmv_hw  # noqa: E402
 
 
+def stencil(rows, points, dtype):
+    """3-D Laplacian-shaped matrix on a g^3 grid (g = rows^(1/3)): 7- or 27-point
+    neighbourhoods, columns sorted within rows, random values. Local columns, but the first two
+    columns of a row lie a grid plane apart."""
+    g = int(round(rows ** (1 / 3)))
+    n = g ** 3
+    idx = np.arange(n, dtype=np.int64)
+    z, y, xx = idx // (g * g), (idx // g) % g, idx % g
+    offs = [(dz, dy, dx) for dz in (-1, 0, 1) for dy in (-1, 0, 1) for dx in (-1, 0, 1)
+            if points == 27 or abs(dz) + abs(dy) + abs(dx) <= 1]
+    cols = np.full((n, len(offs)), -1, np.int64)
+    for k, (dz, dy, dx) in enumerate(offs):  # offsets in increasing column order
+        ok = (z + dz >= 0) & (z + dz < g) & (y + dy >= 0) & (y + dy < g) & (xx + dx >= 0) & (xx + dx < g)
+        cols[ok, k] = idx[ok] + dz * g * g + dy * g + dx
+    lens = (cols >= 0).sum(axis=1)
+    c = cols[cols >= 0].astype(np.uint32)
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    v = np.random.default_rng(2).uniform(-1, 1, len(c)).astype(dtype)
+    t = lambda h: torch.from_numpy(h.view(np.int32) if h.dtype == np.uint32 else h).cuda()
+    return t(rp.astype(np.uint32)), t(c), t(v), n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="powerlaw,banded")
@@ -34,6 +57,9 @@ def main():
         if wl == "banded":
             n = a.rows or 1_000_000
             rp, col, val = spmv_hw.gen_banded(lib, n, 16)
+            x = spmv_hw.gen_vector(lib, n, seed=3)
+        elif wl in ("stencil7", "stencil27"):
+            rp, col, val, n = stencil(a.rows or 8_000_000, 7 if wl == "stencil7" else 27, dtype)
             x = spmv_hw.gen_vector(lib, n, seed=3)
         else:
             n = a.rows or 10_000_000
