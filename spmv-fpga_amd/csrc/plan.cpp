@@ -18,6 +18,8 @@
 
 #include "spmv_internal.hpp"
 
+static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool timing);
+
 namespace spmvhw {
 
 static thread_local std::string g_err;
@@ -88,12 +90,16 @@ struct PhaseTrace {
     }
 };
 
-// Which kernel a plan uses: env SPMV_HW_KERNEL = tiles | sweep | auto (default).
+constexpr int kKernelTune = -2;
+
+// Which kernel a plan uses: env SPMV_HW_KERNEL = tiles | sweep | gold | tune | auto (default).
 static int requested_kernel()
 {
     const char *e = std::getenv("SPMV_HW_KERNEL");
     if (!e || !*e || !std::strcmp(e, "auto"))
         return -1;
+    if (!std::strcmp(e, "tune"))
+        return kKernelTune;
     if (!std::strcmp(e, "tiles"))
         return kKernelTiles;
     if (!std::strcmp(e, "sweep"))
@@ -250,6 +256,59 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
     return 0;
 }
 
+// Builds plan P's layout for `kernel` from the validated device CSR and loads its kernels.
+static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexType *h_row_ptr,
+                        const IndexType *d_col, const ValueType *d_val, hipStream_t s)
+{
+    P.kernel = kernel;
+    if (kernel == kKernelSweep) {
+        const int rc = build_sweep(P, h_row_ptr, d_col, d_val, s);
+        if (rc == 2 && automatic)
+            P.kernel = kernel = kKernelTiles;  // the tile layout has no 32-bit entry-offset limit
+        else if (rc)
+            return 1;
+    }
+    if (kernel == kKernelGold) {
+        if (build_gold(P, h_row_ptr, d_col, d_val, s))
+            return 1;
+    } else if (kernel != kKernelSweep) {
+        if (build_tiles(P, h_row_ptr, d_col, d_val, s))
+            return 1;
+    }
+    SPMV_TRY(hipStreamSynchronize(s));
+    // load the code objects of the kernels this plan launches (no launch; best effort: a
+    // failure here only means the first run loads them)
+    if (P.kernel == kKernelSweep) {
+        (void)launch_sweep(P, nullptr, nullptr, s, true);
+    } else if (P.kernel == kKernelGold) {
+        (void)launch_gold(P, nullptr, nullptr, s, true);
+    } else {
+        (void)launch_spmv(P, nullptr, nullptr, s, true);
+        (void)launch_fixup(P, nullptr, s, true);
+    }
+    (void)hipGetLastError();
+    return 0;
+}
+
+// Mean time of 3 SpMVs (after one warm-up) with scratch x/y, for SPMV_HW_KERNEL=tune.
+static int time_layout(spmv_plan &P, const ValueType *d_x, ValueType *d_y, hipStream_t s, double *ms)
+{
+    hipEvent_t e0, e1;
+    SPMV_TRY(hipEventCreate(&e0));
+    SPMV_TRY(hipEventCreate(&e1));
+    int rc = ::run_impl(&P, d_x, d_y, s, false);
+    (void)hipEventRecord(e0, s);
+    for (int i = 0; i < 3 && !rc; ++i)
+        rc = ::run_impl(&P, d_x, d_y, s, false);
+    (void)hipEventRecord(e1, s);
+    float t = 0.f;
+    if (!rc && hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess)
+        *ms = t / 3.0;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
+
 int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,
                                  const IndexType *h_row_ptr, const IndexType *col_src,
                                  const ValueType *val_src, bool src_on_device, hipStream_t s)
@@ -314,7 +373,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     }
 
     int kernel = requested_kernel();
-    if (kernel < 0) {
+    if (kernel == -1) {
         // automatic choice: the sweep pays once x outgrows ~half an XCD's L2 and the columns of a
         // row are scattered (the first two columns of sampled rows lie >= 64 apart). Measured on
         // power-law matrices with 16 nnz/row (profiles/r01_ab_variants.jsonl): tie at x = 1.6 MB,
@@ -330,43 +389,44 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
                 kernel = kKernelSweep;
         }
     }
-    p->kernel = kernel;
     trace("validate + kernel choice", s);
     if (const char *t = std::getenv("SPMV_SWEEP_THREADS")) {
         const int v = std::atoi(t);
         if (v == 256 || v == 512 || v == 1024)
             p->sweep_threads = v;
     }
-    if (kernel == kKernelSweep) {
-        const int rc = build_sweep(*p, h_row_ptr, d_col, d_val, s);
-        if (rc == 2 && requested_kernel() != kKernelSweep) {
-            p->kernel = kernel = kKernelTiles;  // automatic choice: the tile layout has no such limit
-        } else if (rc) {
+    if (kernel == kKernelTune) {
+        // build both layouts, time one SpMV of each on this matrix, keep the faster
+        std::unique_ptr<spmv_plan> q(new spmv_plan());
+        q->device = p->device;
+        q->nr_rows = p->nr_rows;
+        q->nr_cols = p->nr_cols;
+        q->nnz = p->nnz;
+        q->nzr = p->nzr;
+        q->has_empty = p->has_empty;
+        q->sweep_threads = p->sweep_threads;
+        if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s) ||
+            build_layout(*q, kKernelSweep, true, h_row_ptr, d_col, d_val, s))
             return 1;
-        }
-    }
-    if (kernel == kKernelGold) {
-        if (build_gold(*p, h_row_ptr, d_col, d_val, s))
+        Tmp tx, ty;
+        SPMV_TRY(hipMalloc(&tx.p, std::max<size_t>(nr_cols, 1) * sizeof(ValueType)));
+        SPMV_TRY(hipMalloc(&ty.p, std::max<size_t>(nr_rows, 1) * sizeof(ValueType)));
+        SPMV_TRY(hipMemsetAsync(tx.p, 0, std::max<size_t>(nr_cols, 1) * sizeof(ValueType), s));
+        double mt = 1e30, ms = 1e30;
+        if (time_layout(*p, (const ValueType *)tx.p, (ValueType *)ty.p, s, &mt) ||
+            time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ms))
             return 1;
-    } else if (kernel != kKernelSweep) {
-        if (build_tiles(*p, h_row_ptr, d_col, d_val, s))
-            return 1;
-    }
-    SPMV_TRY(hipStreamSynchronize(s));
-    trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelGold ? "build gold layout"
-                                                                                    : "build tile layout", s);
-    // load the code objects of the kernels this plan launches (no launch; best effort: a
-    // failure here only means the first run loads them)
-    if (p->kernel == kKernelSweep) {
-        (void)launch_sweep(*p, nullptr, nullptr, s, true);
-    } else if (p->kernel == kKernelGold) {
-        (void)launch_gold(*p, nullptr, nullptr, s, true);
+        if (ms < mt)
+            p.swap(q);
+        p->tuned_ms[0] = mt;
+        p->tuned_ms[1] = ms;
+        trace("tune: build both + time", s);
     } else {
-        (void)launch_spmv(*p, nullptr, nullptr, s, true);
-        (void)launch_fixup(*p, nullptr, s, true);
+        if (build_layout(*p, kernel, requested_kernel() < 0, h_row_ptr, d_col, d_val, s))
+            return 1;
+        trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelGold ? "build gold layout"
+                                                                                        : "build tile layout", s);
     }
-    (void)hipGetLastError();
-    trace("load kernels", s);
     *out = p.release();
     return 0;
 }

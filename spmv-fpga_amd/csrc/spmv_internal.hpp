@@ -95,6 +95,7 @@ struct spmv_plan {
     bool sweep_packed = false;
     bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)
     double locality = -1.0;    // probe result used by the automatic kernel choice
+    double tuned_ms[2] = {-1.0, -1.0};  // SPMV_HW_KERNEL=tune: measured tiles / sweep ms
 
     // timing (HIP events around the main kernel, on the launch stream)
     bool timing = false;

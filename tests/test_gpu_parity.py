@@ -482,6 +482,29 @@ def test_dense_rows_among_short_ones(torch, monkeypatch, kern):
         check(row_ptr, col, val, x, ref, y, np.float64)
 
 
+@pytest.mark.parametrize("workload,want", [("powerlaw", 2), ("banded", 0)])
+def test_tune_mode_keeps_the_faster_layout(torch, monkeypatch, workload, want):
+    """SPMV_HW_KERNEL=tune builds both layouts, times them on the matrix and keeps the faster:
+    the sweep for scattered columns, the tiles for a band."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "tune")
+    lib = spmv_hw.load(np.float64)
+    n = 2_000_000
+    if workload == "powerlaw":
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 16 * n, seed=4)
+    else:
+        rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    assert plan.stats()["kernel"] == want
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    h = [t.cpu().numpy() for t in (rp, col, val, x, y)]
+    row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
+    check(row_ptr, c, v, xx, oracle.spmv_gold(row_ptr, c, v, xx), yy, np.float64)
+    plan.destroy()
+
+
 def test_auto_kernel_choice(torch, monkeypatch):
     """Automatic choice: banded (local columns) -> tiles; power-law with columns spread over an x
     much larger than the L2s -> sweep."""
