@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
+    ap.add_argument("--no-strong-companion", action="store_true",
+                    help="N > 1 weak runs: skip the config-4 strong-scaling companion measurement")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the row-parallel CPU line (the box's CPU share is 16)")
@@ -172,6 +174,56 @@ def cpu_baseline(lib, rp, col, val, x, y_gpu, reps, args_threads=16):
     parity = {"max_scaled_err": err, "tol": 1e-6 if h_val.dtype == np.float64 else 1e-4,
               "ref_abs_1e-5_errors": abs_errors, "pass": bool(err <= (1e-6 if h_val.dtype == np.float64 else 1e-4))}
     return base, parity
+
+
+def strong_companion(lib, args, world, rank, dev, stream):
+    """Config 4 beside a weak-scaling run: the SAME 10M/160M matrix cut into `world` nnz-balanced
+    row slices (one per rank), timed like the headline (warm-up, barrier-bracketed K steps, max
+    over ranks), plus the RCCL y exchange of its slices: reduce of full-length partials (the
+    accum_results '+=' mapping) and gather of the disjoint slices."""
+    import copy
+    a = copy.copy(args)
+    a.scaling = "strong"
+    rp, col, val, x, ncols, desc = build_workload(lib, a, world, rank)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, ncols, device=dev.index, stream=stream)
+    st = plan.stats()
+    del rp, col, val
+    y = torch.empty(st["nr_rows"], dtype=x.dtype, device=dev)
+    for _ in range(args.warmup):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    ms = spmv_dist.max_over_ranks((time.perf_counter() - t0) * 1e3 / args.steps, dev)
+    nnz_all = spmv_dist.sum_over_ranks([float(st["nr_nzeros"])], dev)[0]
+    cnt = [0.0] * world
+    cnt[rank] = float(st["nr_rows"])
+    counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
+    row_begin, n_total = int(counts[:rank].sum()), int(counts.sum())
+    res = {"n_gpus": world, "value": round(2.0 * nnz_all / (ms * 1e-3) / 1e9, 3), "unit": "GFLOP/s",
+           "ms_per_step": round(ms, 5), "slice_rows": desc.get("slice_rows"), "kernel": st["kernel"],
+           "units": st["nr_tiles"]}
+    for mode in ("reduce", "gather"):
+        def exchange():
+            return (spmv_dist.exchange_reduce(y, row_begin, n_total) if mode == "reduce"
+                    else spmv_dist.exchange_gather(y, counts))
+        exchange()
+        torch.cuda.synchronize()
+        barrier(world)
+        te0 = time.perf_counter()
+        for _ in range(3):
+            exchange()
+        torch.cuda.synchronize()
+        barrier(world)
+        res[f"{mode}_ms"] = round(spmv_dist.max_over_ranks((time.perf_counter() - te0) * 1e3 / 3, dev), 4)
+    res["e2e_gflops_with_reduce"] = round(2.0 * nnz_all / ((ms + res["reduce_ms"]) * 1e-3) / 1e9, 2)
+    res["e2e_gflops_with_gather"] = round(2.0 * nnz_all / ((ms + res["gather_ms"]) * 1e-3) / 1e9, 2)
+    plan.destroy()
+    return res
 
 
 def main():
@@ -330,6 +382,10 @@ def main():
         res["e2e_gflops_with_gather"] = round(2.0 * nnz_all / ((ms + res["gather_ms"]) * 1e-3) / 1e9, 2)
         exchange = res
 
+    strong = None
+    if world > 1 and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
+        strong = strong_companion(lib, args, world, rank, dev, stream)
+
     cpu = None
     parity = None
     if keep_csr:
@@ -362,6 +418,7 @@ def main():
             "parity": parity,
             "exchange": exchange,
             "graph": graph,
+            "strong_companion": strong,
             "host_copy": host,
             "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
             "setup_s": round(setup_s, 2),
