@@ -303,11 +303,15 @@ def main():
     gflops = 2.0 * nnz_all / (ms * 1e-3) / 1e9
     eff_gbps = alg_all / (ms * 1e-3) / 1e9
     # roofline of the dominant kernel: algorithmic bytes of one launch / mean launch duration
+    # (max over ranks: every rank's dominant kernel has the same per-launch algorithmic bytes)
+    kernel_ms = kernel_ms_max
     achieved = alg_local / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     # the dominant kernel of this plan; its PMC traffic is taken from profiles/traffic.json only
     # when that summary was recorded for the same workload, size and kernel
     if st["kernel"] == 2:
         kname = "k_spmv_sweep_packed" if st["format"] & 2 else "k_spmv_sweep"
+    elif st["kernel"] == 1:
+        kname = "k_spmv_gold"
     else:
         kname = "k_spmv_tiles"
     traffic = None
