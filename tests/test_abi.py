@@ -169,3 +169,26 @@ def test_dropin_header_compiles_and_links_against_caller_types(tmp_path):
     subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
                     "-o", str(exe), "-L", lib_dir, "-lspmv_hw_f64", f"-Wl,-rpath,{lib_dir}"], check=True)
     assert exe.exists()
+
+
+def test_part2_argument_errors_return_codes_without_a_gpu():
+    """Part 2 reports bad arguments through its return code and spmv_hw_last_error() (the
+    reference has no error channel; Part 1 exits instead). None of these reach a HIP call."""
+    lib = spmv_hw.load(np.float64)
+    L = lib.L
+    cases = [
+        (lambda: L.spmv_plan_create_device(None, 0, 4, 4, 0, None, None, None, None), "null argument"),
+        (lambda: L.spmv_plan_run(None, None, None, None), "null plan"),
+        (lambda: L.spmv_plan_run_graph(None, None, None, 1, None), "iters"),
+        (lambda: L.spmv_plan_get_stats(None, None), "null argument"),
+        (lambda: L.spmv_plan_set_variant(None, 0), "bad arguments"),
+        (lambda: L.spmv_plan_set_timing(None, 1), "null plan"),
+        (lambda: L.spmv_partition_rows(None, 0, 1, None), "bad arguments"),
+    ]
+    for call, msg in cases:
+        assert call() == 1
+        assert msg in L.spmv_hw_last_error().decode()
+    rp = np.array([0, 1], np.uint32)
+    bounds = np.zeros(1, np.uint32)
+    assert L.spmv_partition_rows(rp.ctypes.data_as(ctypes.POINTER(spmv_hw.IndexType)), 1, 0,
+                                 bounds.ctypes.data_as(ctypes.POINTER(spmv_hw.IndexType))) == 1

@@ -195,6 +195,21 @@ def test_out_of_range_column_is_rejected(torch, kernel):
                                  to_dev(torch, np.ones(2)), 5)
 
 
+def test_malformed_row_ptr_and_variant_are_rejected(torch, kernel):
+    lib = spmv_hw.load(np.float64)
+    row_ptr = np.array([0, 3, 2, 4], np.uint32)  # decreasing at row 1
+    col = np.array([0, 1, 2, 3], np.uint32)
+    with pytest.raises(RuntimeError, match="non-decreasing"):
+        spmv_hw.Plan.from_device(lib, to_dev(torch, row_ptr), to_dev(torch, col), to_dev(torch, np.ones(4)), 4)
+    plan = spmv_hw.Plan.from_device(lib, to_dev(torch, np.array([0, 2, 4], np.uint32)), to_dev(torch, col),
+                                    to_dev(torch, np.ones(4)), 4)
+    with pytest.raises(RuntimeError, match="bad arguments"):
+        plan.set_variant(64)
+    with pytest.raises(RuntimeError, match="iters"):
+        plan.run_graph(to_dev(torch, np.ones(4)), torch.empty(2, dtype=torch.float64, device="cuda"), 0)
+    plan.destroy()
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_deterministic(torch, kernel, dtype):
     """The tile kernel is bitwise reproducible (partials added in a fixed order). The sweep kernel
