@@ -86,10 +86,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     const V *__restrict__ val, const uint32_t *__restrict__ rowend,
     const uint32_t *__restrict__ tile_info, const uint32_t *__restrict__ row_id,
     const V *__restrict__ x, V *__restrict__ y, V *__restrict__ head, V *__restrict__ tail,
-    uint64_t nnz, uint64_t ntiles)
+    uint64_t nnz, uint64_t ntiles, uint32_t xcd_chunk)
 {
     const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t t = (uint64_t)blockIdx.x * (kBlockThreads / kWave) + (threadIdx.x >> 6);
+    // XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin, so workgroup b runs
+    // on XCD b % 8; with xcd_chunk > 0 that XCD takes the contiguous block range
+    // [(b % 8) * xcd_chunk, +xcd_chunk) in order, and rows that share x lines (neighbouring
+    // tiles) meet in one XCD's L2 instead of being fetched by all eight
+    const uint64_t blk = xcd_chunk ? (uint64_t)(blockIdx.x % 8u) * xcd_chunk + blockIdx.x / 8u : blockIdx.x;
+    const uint64_t t = blk * (kBlockThreads / kWave) + (threadIdx.x >> 6);
     if (t >= ntiles)
         return;  // wave-uniform
     const uint64_t k0 = t * (uint64_t)(U * kStep);
@@ -245,12 +250,14 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
     if (p.ntiles == 0)
         return hipSuccess;
     const uint64_t waves_per_block = kBlockThreads / kWave;
-    const uint64_t blocks = (p.ntiles + waves_per_block - 1) / waves_per_block;
+    const uint64_t nblk = (p.ntiles + waves_per_block - 1) / waves_per_block;
+    const uint32_t xcd_chunk = p.tile_xcd ? (uint32_t)((nblk + 7) / 8) : 0u;
+    const uint64_t blocks = xcd_chunk ? 8ull * xcd_chunk : nblk;
 #define SPMV_LAUNCH(VAR, CB)                                                                      \
     launch_or_warm(warm, k_spmv_tiles<ValueType, kTileSteps, VAR, CB>, dim3((unsigned)blocks),       \
                        dim3(kBlockThreads), 0, s, p.d_col, p.d_colnar, p.d_tile_cbase, p.d_val,     \
                        p.d_rowend, p.d_tile_info, p.d_row_id, d_x, d_y, p.d_head, p.d_tail, p.nnz, \
-                       p.ntiles)
+                       p.ntiles, xcd_chunk)
 #define SPMV_VARIANTS(CB)                    \
     switch (p.variant & 3) {                 \
     case 0: SPMV_LAUNCH(0, CB); break;       \

@@ -79,6 +79,9 @@ def main():
                 if kern.endswith("F"):  # sweep with split panels whenever they fit
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_SPLIT"] = "2"
+                if kern.endswith("R"):  # tile kernel with round-robin (not XCD-contiguous) tiles
+                    kern = kern[:-1]
+                    os.environ["SPMV_TILE_XCD"] = "0"
                 if kern.endswith("H"):  # tile kernel with at most 16-bit column offsets
                     kern = kern[:-1]
                     os.environ["SPMV_TILE_NARROW"] = "16"
@@ -97,6 +100,7 @@ def main():
                 os.environ.pop("SPMV_SWEEP_LANE_ORDER", None)
                 os.environ.pop("SPMV_TILE_NARROW", None)
                 os.environ.pop("SPMV_SWEEP_SPLIT", None)
+                os.environ.pop("SPMV_TILE_XCD", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
