@@ -221,7 +221,7 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
     if (p.nnz_pad)
         SPMV_TRY(launch_pack(d_col_src, d_val_src, nnz, p.nnz_pad, p.nr_cols, p.d_col, p.d_val, nullptr, s));
     if (const char *xe = std::getenv("SPMV_TILE_XCD"))
-        p.tile_xcd = xe[0] != '0';
+        p.tile_xcd = xe[0] == '1';
     // narrow form: 8- or 16-bit column offsets from a per-tile base when every tile allows it
     // (env SPMV_TILE_NARROW: 0 = keep 32-bit columns, 16 = at most 16-bit, default narrowest)
     const char *nenv = std::getenv("SPMV_TILE_NARROW");

@@ -79,9 +79,9 @@ def main():
                 if kern.endswith("F"):  # sweep with split panels whenever they fit
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_SPLIT"] = "2"
-                if kern.endswith("R"):  # tile kernel with round-robin (not XCD-contiguous) tiles
+                if kern.endswith("X"):  # tile kernel with XCD-contiguous (not round-robin) tiles
                     kern = kern[:-1]
-                    os.environ["SPMV_TILE_XCD"] = "0"
+                    os.environ["SPMV_TILE_XCD"] = "1"
                 if kern.endswith("H"):  # tile kernel with at most 16-bit column offsets
                     kern = kern[:-1]
                     os.environ["SPMV_TILE_NARROW"] = "16"
