@@ -550,6 +550,10 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         set_error("build_sweep: padded entry count exceeds 32 bits");
         return 2;
     }
+    if (nnz > 0x7FFFFFFFull) {  // hipcub's radix sort takes an int item count
+        set_error("build_sweep: more than 2^31-1 non-zeros in one slice");
+        return 2;
+    }
     p.npanels = P;
     p.panel_rmax = rmax_used;
     p.ent_pad = poff[P];
