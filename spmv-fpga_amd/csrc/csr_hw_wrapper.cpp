@@ -149,14 +149,16 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         spmv_plan_get_stats(h->plan, &st);
         const spmv_plan &pl = *h->plan;
         const bool sweep = pl.kernel == kKernelSweep;
-        const uint64_t val_bytes = (sweep ? pl.ent_pad : pl.nnz_pad) * sizeof(ValueType);
+        // stored entries of the representation (padded for tiles and sweep, plain for gold)
+        const uint64_t stored = sweep ? pl.ent_pad : pl.kernel == kKernelGold ? pl.nnz : pl.nnz_pad;
+        const uint64_t val_bytes = stored * sizeof(ValueType);
         // the index stream of the unit's representation (opaque device address)
         h->sub[0] = sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)
                     : pl.tile_col_bytes < 4 ? reinterpret_cast<BusDataType *>(pl.d_colnar)
                                      : reinterpret_cast<BusDataType *>(pl.d_col);
         h->nr_rows[0] = (IndexType)st.nr_nonempty_rows;
         h->nr_cols[0] = matrix->nr_cols;
-        h->nr_nzeros[0] = (IndexType)(sweep ? pl.ent_pad : pl.nnz_pad);
+        h->nr_nzeros[0] = (IndexType)stored;
         h->nr_ci[0] = (IndexType)ceil16(st.device_bytes - val_bytes);
         h->nr_val[0] = (IndexType)ceil16(val_bytes);
         h->pub.submatrix = h->sub;
