@@ -74,10 +74,21 @@ struct hw_vector_impl {
 };
 
 hw_matrix_impl *impl(csr_hw_matrix *m) { return reinterpret_cast<hw_matrix_impl *>(m); }
+
+// The unit arrays (hw_matrix, hw_y) carry one extra null entry, so every call knows the unit
+// count of the matrix it was given (several matrices with different SPMV_NGPUS may coexist).
+template <typename T>
+int units_of(T **arr)
+{
+    int u = 0;
+    while (arr[u])
+        ++u;
+    return u;
+}
 hw_vector_impl *impl(csr_hw_vector *v) { return reinterpret_cast<hw_vector_impl *>(v); }
 
 std::mutex g_mu;
-int g_units_in_use = 0;                 // units of the most recent create_csr_hw_matrix
+int g_units_max = 0;                    // most units of any create_csr_hw_matrix so far (x upload)
 std::vector<hipStream_t> g_streams;     // one stream per unit
 
 hipStream_t unit_stream(int unit)
@@ -121,7 +132,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
     if (spmv_partition_rows(matrix->row_ptr, n, units, bounds.data()))
         die(spmv_hw_last_error());
 
-    *hw_matrix = (csr_hw_matrix **)std::malloc(units * sizeof(csr_hw_matrix *));
+    *hw_matrix = (csr_hw_matrix **)std::calloc(units + 1, sizeof(csr_hw_matrix *));
     uint64_t in_bytes = 0, nnz_total = 0;
     for (int u = 0; u < units; ++u) {
         auto *h = new hw_matrix_impl();
@@ -174,7 +185,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
     }
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        g_units_in_use = units;
+        g_units_max = std::max(g_units_max, units);
     }
     // empty_rows_bitmap[block][row] (csr_hw.cpp:391-393, :340-347): inner rows live inside the
     // outer allocation, so the caller's free(outer) (main.cpp:95) releases all of it.
@@ -198,8 +209,8 @@ void create_csr_hw_y_vector(csr_hw_matrix **hw_matrix, csr_hw_vector ***hw_vecto
 {
     if (!hw_matrix || !hw_vector)
         die("create_csr_hw_y_vector: null argument");
-    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
-    *hw_vector = (csr_hw_vector **)std::malloc(units * sizeof(csr_hw_vector *));
+    const int units = units_of(hw_matrix);
+    *hw_vector = (csr_hw_vector **)std::calloc(units + 1, sizeof(csr_hw_vector *));
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
         auto *v = new hw_vector_impl();
@@ -229,7 +240,7 @@ void create_csr_hw_x_vector(csr_hw_vector **hw_x, csr_vector *x, int blocks, Ind
         die("create_csr_hw_x_vector: blocks must be hw_matrix[0]->blocks (1)");
     if (x->nr_values > nr_cols[0])
         die("create_csr_hw_x_vector: x is longer than the matrix has columns");
-    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    const int units = std::max(g_units_max, spmv_hw_units());
     const int ndev = std::min(units, device_count());
     auto *v = new hw_vector_impl();
     v->per_device.assign(ndev, nullptr);
@@ -257,7 +268,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
     (void)empty_rows_bitmap;  // the device representation carries its own row map
     if (!hw_matrix || !hw_x || !y_fpga)
         die("spmv_hw: null argument");
-    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    const int units = units_of(hw_matrix);
     hw_vector_impl *x = impl(hw_x);
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
@@ -349,7 +360,7 @@ void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix)
 {
     if (!hw_matrix)
         return;
-    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    const int units = units_of(hw_matrix);
     for (int u = 0; u < units; ++u) {
         if (!hw_matrix[u])
             continue;
@@ -386,7 +397,7 @@ void delete_csr_hw_y_vector(csr_hw_vector **hw_vector)
 {
     if (!hw_vector)
         return;
-    const int units = g_units_in_use > 0 ? g_units_in_use : spmv_hw_units();
+    const int units = units_of(hw_vector);
     for (int u = 0; u < units; ++u)
         delete_vector(hw_vector[u]);
     std::free(hw_vector);

@@ -145,6 +145,38 @@ def test_reference_api_flow(torch, monkeypatch, kernel, name, dtype, tag, units)
     lib.delete_csr_hw_x_vector(hx)
 
 
+def test_two_matrices_with_different_unit_counts_coexist(torch, monkeypatch):
+    """Each hw_matrix array knows its own unit count (null-terminated), so matrices created
+    under different SPMV_NGPUS can be used and deleted in any order; create_csr_hw_y_vector
+    follows the matrix it is given."""
+    lib = spmv_hw.load(np.float64)
+    mats = []
+    for units, name in ((3, "small"), (1, "longrow")):
+        monkeypatch.setenv("SPMV_NGPUS", str(units))
+        path = os.path.join(GOLDEN, manifest()[name]["file"])
+        r, c, row_ptr, col, val, _ = oracle.read_csr(path, np.float64)
+        x, y_gold = golden_arrays(name, "f64")
+        m = lib.make_csr_matrix(row_ptr, col, val, c)
+        hw, bm = lib.create_csr_hw_matrix(m)
+        hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(x), 1, hw[0].contents.nr_cols)
+        mats.append((units, r, hw, bm, hx, y_gold, m))
+    for units, r, hw, bm, hx, y_gold, _ in mats[::-1]:
+        count = 0
+        while hw[count]:  # the array ends with a null entry
+            count += 1
+        assert count == units
+        hy = lib.create_csr_hw_y_vector(hw)
+        lib.delete_csr_hw_y_vector(hy)
+        yv = lib.make_csr_vector(np.zeros(r))
+        lib.spmv_hw(hw, hx, yv, bm)
+        y = np.ctypeslib.as_array(yv.values, shape=(r,))
+        assert lib.verification(y_gold, y.copy()) == 0
+    for _, _, hw, bm, hx, _, _ in mats:
+        lib.delete_csr_hw_matrix(hw)
+        lib.free_bitmap(bm)
+        lib.delete_csr_hw_x_vector(hx)
+
+
 EDGE_CASES = {
     # name: (n, m, lengths-builder)
     "tile_aligned_rows": (64, 4096, lambda rng: np.full(64, 512)),
