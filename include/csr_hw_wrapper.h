@@ -83,8 +83,9 @@ typedef struct spmv_plan_stats {
                                     layouts, time them on the matrix, keep the faster) */
     int32_t blocks;              /* column blocks of the representation */
     int32_t format;              /* bit 0: 16- or 8-bit column offsets per tile (kernel 0), bit 3:
-                                    8-bit; bit 1: packed 12/8-byte sweep entries; bit 2:
-                                    lane-ordered chunks (kernel 2) */
+                                    8-bit, bit 4: 16-bit (cluster, offset) with 4 bases per tile;
+                                    bit 1: packed 12/8-byte sweep entries; bit 2: lane-ordered
+                                    chunks (kernel 2) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are

@@ -79,7 +79,9 @@ __device__ __forceinline__ void emit(V sum, uint32_t r, bool to_head, V *__restr
 
 // VAR bit 0: non-temporal streamed loads (col, val, row-end bits); bit 1: non-temporal y stores.
 // CB = bytes per stored column: 4 = absolute (col), 2 / 1 = offsets (colnar) from the tile's
-// base column (tile_cbase).
+// base column (tile_cbase); CB = 3 = clustered 16-bit: (cluster << 14) | offset from one of the
+// tile's four bases (tile_cbase[4 t + cluster]), for tiles whose columns fall into up to four
+// narrow clusters (3-D stencils: one cluster per grid plane).
 template <typename V, int U, int VAR, int CB>
 __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     const uint32_t *__restrict__ col, const void *__restrict__ colnar, const uint32_t *__restrict__ tile_cbase,
@@ -103,13 +105,28 @@ __global__ __launch_bounds__(kBlockThreads) void k_spmv_tiles(
     uint32_t c[U][4];
     V v[U][4];
     uint32_t fl[U];
-    const uint32_t cbase = CB < 4 ? tile_cbase[t] : 0u;
+    const uint32_t cbase = (CB == 1 || CB == 2) ? tile_cbase[t] : 0u;
+    uint32_t cb4[4] = {0u, 0u, 0u, 0u};
+    if constexpr (CB == 3) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            cb4[k] = tile_cbase[4 * t + k];  // wave-uniform: scalar loads
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t kb = k0 + (uint64_t)u * kStep;
         if constexpr (CB == 2) {
             const u16x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u16x4 *>(colnar) + (kb / 4 + lane));
             c[u][0] = cbase + cc.x; c[u][1] = cbase + cc.y; c[u][2] = cbase + cc.z; c[u][3] = cbase + cc.w;
+        } else if constexpr (CB == 3) {
+            const u16x4 cc = ld<(VAR & 1) != 0>(reinterpret_cast<const u16x4 *>(colnar) + (kb / 4 + lane));
+            const uint32_t w4[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = w4[j] >> 14;
+                const uint32_t b = k == 0 ? cb4[0] : k == 1 ? cb4[1] : k == 2 ? cb4[2] : cb4[3];
+                c[u][j] = b + (w4[j] & 0x3FFFu);
+            }
         } else if constexpr (CB == 1) {
             const uint32_t cc = ld<(VAR & 1) != 0>(reinterpret_cast<const uint32_t *>(colnar) + (kb / 4 + lane));
             c[u][0] = cbase + (cc & 0xFFu); c[u][1] = cbase + ((cc >> 8) & 0xFFu);
@@ -267,6 +284,8 @@ hipError_t launch_spmv(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
     }
     if (p.tile_col_bytes == 1) {
         SPMV_VARIANTS(1)
+    } else if (p.tile_col_bytes == 2 && p.tile_clustered) {
+        SPMV_VARIANTS(3)
     } else if (p.tile_col_bytes == 2) {
         SPMV_VARIANTS(2)
     } else {
@@ -346,6 +365,69 @@ __global__ __launch_bounds__(256) void k_tile_span(const uint32_t *__restrict__ 
     }
 }
 
+// One wave per tile: up to four cluster bases. base_0 = the tile's min column; base_k = the min
+// column >= base_{k-1} + 16384. Every column then lies within 16384 of the largest base not
+// above it, unless some column is >= base_3 + 16384 (*bad |= 1: the plan keeps 32-bit columns).
+__global__ __launch_bounds__(256) void k_tile_clusters(const uint32_t *__restrict__ col, uint64_t nnz, uint64_t ntiles,
+                                                       uint32_t *__restrict__ bases, uint32_t *__restrict__ bad)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= ntiles)
+        return;
+    uint32_t cols[kTileNnz / kWave];
+#pragma unroll
+    for (int j = 0; j < kTileNnz / kWave; ++j) {
+        const uint64_t k = t * kTileNnz + (uint64_t)j * kWave + lane;
+        cols[j] = k < nnz ? col[k] : 0xFFFFFFFFu;  // padding: not a column
+    }
+    uint64_t lim = 0;  // next base = min column >= lim
+    uint32_t base[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < kTileNnz / kWave; ++j)
+            if (cols[j] != 0xFFFFFFFFu && cols[j] >= lim && cols[j] < m)
+                m = cols[j];
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t o = __shfl_xor(m, d, kWave);
+            m = o < m ? o : m;
+        }
+        base[b] = m == 0xFFFFFFFFu ? (b ? base[b - 1] : 0u) : m;
+        lim = m == 0xFFFFFFFFu ? lim : uint64_t(m) + 16384u;
+    }
+    bool over = false;
+#pragma unroll
+    for (int j = 0; j < kTileNnz / kWave; ++j)
+        over |= cols[j] != 0xFFFFFFFFu && uint64_t(cols[j]) >= lim;
+    if (__ballot(over) && lane == 0)
+        atomicOr(bad, 1u);
+    if (lane < 4)
+        bases[4 * t + lane] = base[lane];
+}
+
+__global__ void k_cluster_encode(const uint32_t *__restrict__ col, uint64_t nnz, uint64_t nnz_pad,
+                                 const uint32_t *__restrict__ bases, uint16_t *__restrict__ out)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz_pad)
+        return;
+    const uint32_t *b = bases + 4 * (k / kTileNnz);
+    if (k >= nnz) {
+        out[k] = 0;  // padding: gathers x[base_0] with value 0 and no row end
+        return;
+    }
+    const uint32_t c = col[k];
+    uint32_t cl = 0;
+#pragma unroll
+    for (uint32_t j = 1; j < 4; ++j)
+        if (b[j] <= c && b[j] > b[j - 1])
+            cl = j;
+    out[k] = (uint16_t)((cl << 14) | (c - b[cl]));
+}
+
 template <typename T>
 __global__ void k_narrow(const uint32_t *__restrict__ col, uint64_t nnz, uint64_t nnz_pad,
                          const uint32_t *__restrict__ cbase, T *__restrict__ out)
@@ -364,6 +446,26 @@ hipError_t launch_tile_span(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles
         return hipSuccess;
     hipLaunchKernelGGL(k_tile_span, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, d_col, nnz, ntiles,
                        d_cbase, d_maxspan);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_clusters(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles, uint32_t *d_bases,
+                                uint32_t *d_bad, hipStream_t s)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_tile_clusters, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, d_col, nnz, ntiles,
+                       d_bases, d_bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_cluster_encode(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_bases,
+                                 uint16_t *d_out, hipStream_t s)
+{
+    if (nnz_pad == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_cluster_encode, dim3((unsigned)((nnz_pad + 255) / 256)), dim3(256), 0, s, d_col, nnz,
+                       nnz_pad, d_bases, d_out);
     return hipGetLastError();
 }
 

@@ -251,6 +251,35 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
         } else {
             SPMV_TRY(hipFree(p.d_tile_cbase));
             p.d_tile_cbase = nullptr;
+            // clustered 16-bit columns: up to four narrow column clusters per tile
+            const char *cenv = std::getenv("SPMV_TILE_CLUSTER");
+            if (!(cenv && cenv[0] == '0')) {
+                uint32_t *d_bad = nullptr;
+                SPMV_TRY(alloc((void **)&p.d_tile_cbase, p.ntiles * 4 * sizeof(uint32_t)));
+                SPMV_TRY(alloc((void **)&d_bad, sizeof(uint32_t)));
+                uint32_t bad = 1;
+                e = hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s);
+                if (e == hipSuccess)
+                    e = launch_tile_clusters(p.d_col, nnz, p.ntiles, p.d_tile_cbase, d_bad, s);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess)
+                    e = hipStreamSynchronize(s);
+                (void)hipFree(d_bad);
+                SPMV_TRY(e);
+                if (!bad) {
+                    SPMV_TRY(alloc(&p.d_colnar, p.nnz_pad * 2));
+                    SPMV_TRY(launch_cluster_encode(p.d_col, nnz, p.nnz_pad, p.d_tile_cbase, (uint16_t *)p.d_colnar, s));
+                    SPMV_TRY(hipStreamSynchronize(s));
+                    SPMV_TRY(hipFree(p.d_col));
+                    p.d_col = nullptr;
+                    p.tile_col_bytes = 2;
+                    p.tile_clustered = true;
+                } else {
+                    SPMV_TRY(hipFree(p.d_tile_cbase));
+                    p.d_tile_cbase = nullptr;
+                }
+            }
         }
     }
     // pageable host vectors above go out of scope: make the copies complete first
@@ -464,7 +493,7 @@ uint64_t spmv_plan::device_bytes() const
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
                (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * 8 : 0) + nunits * 4 + (npanels + 1) * 4;
     return nnz_pad * (tile_col_bytes + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
-           (tile_col_bytes < 4 ? ntiles * 4 : 0) +
+           (tile_col_bytes < 4 ? ntiles * (tile_clustered ? 16 : 4) : 0) +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;
 }
 
@@ -643,7 +672,7 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->kernel = p->kernel;
     st->blocks = 1;
     st->format = (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) |
-                 (p->tile_col_bytes == 1 ? 8 : 0);
+                 (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0);
     return 0;
 }
 

@@ -64,6 +64,7 @@ struct spmv_plan {
     void *d_colnar = nullptr;        // narrow form: u16 or u8 offsets from tile_cbase (d_col freed)
     uint32_t *d_tile_cbase = nullptr;
     int tile_col_bytes = 4;          // 4 (d_col), 2 or 1 (d_colnar)
+    bool tile_clustered = false;     // 2-byte columns as (cluster << 14) | offset, 4 bases per tile
     bool tile_xcd = false;           // XCD-contiguous tile order (env SPMV_TILE_XCD=1); measured
                                      // slower on stencils (+6 %), 2 % faster on banded
     ValueType *d_val = nullptr;
@@ -145,6 +146,11 @@ hipError_t launch_validate(const IndexType *d_col, uint64_t nnz, uint32_t ncols,
 // (max column - min column)
 hipError_t launch_tile_span(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles, uint32_t *d_cbase,
                             uint32_t *d_maxspan, hipStream_t s);
+// up to 4 cluster bases per tile (bases u32[4 ntiles]); *d_bad |= 1 when a tile needs more
+hipError_t launch_tile_clusters(const uint32_t *d_col, uint64_t nnz, uint64_t ntiles, uint32_t *d_bases,
+                                uint32_t *d_bad, hipStream_t s);
+hipError_t launch_cluster_encode(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_bases,
+                                 uint16_t *d_out, hipStream_t s);
 // col - cbase[tile] as `bytes`-wide offsets (2 or 1)
 hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, const uint32_t *d_cbase,
                          void *d_out, int bytes, hipStream_t s);

@@ -347,6 +347,7 @@ def test_narrow_tiles_span_limit(torch, monkeypatch, span, narrow):
     < 65536 -> 16-bit, else 32-bit columns."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
     monkeypatch.delenv("SPMV_TILE_NARROW", raising=False)
+    monkeypatch.setenv("SPMV_TILE_CLUSTER", "0")  # the plain narrow limits (clusters: below)
     lib = spmv_hw.load(np.float64)
     m = 70_000
     rng = np.random.default_rng(5)
@@ -550,6 +551,40 @@ def test_tune_mode_keeps_the_faster_layout(torch, monkeypatch, workload, want):
     row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
     check(row_ptr, c, v, xx, oracle.spmv_gold(row_ptr, c, v, xx), yy, np.float64)
     plan.destroy()
+
+
+def _clustered_rows(n, gaps):
+    """Row i has columns i + g for g in gaps (sorted): len(gaps) far-apart column clusters per
+    tile, like a 3-D stencil's grid planes."""
+    row_ptr = (np.arange(n + 1) * len(gaps)).astype(np.uint32)
+    col = (np.arange(n)[:, None] + np.array(gaps)[None, :]).reshape(-1).astype(np.uint32)
+    return row_ptr, col
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("gaps,clustered", [((0, 100_000, 200_000), True),
+                                            ((0, 70_000, 140_000, 210_000), True),
+                                            ((0, 50_000, 100_000, 150_000, 200_000), False)])
+def test_clustered_tile_columns(torch, monkeypatch, dtype, gaps, clustered):
+    """Tiles whose columns fall into <= 4 narrow clusters store 16-bit (cluster, offset)
+    columns; bitwise the same y as 32-bit columns; 5 clusters keep 32-bit columns."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
+    monkeypatch.delenv("SPMV_TILE_NARROW", raising=False)
+    rng = np.random.default_rng(21)
+    n = 60_000
+    row_ptr, col = _clustered_rows(n, gaps)
+    m = int(col.max()) + 1
+    val = rng.uniform(-1, 1, len(col)).astype(dtype)
+    x = rng.uniform(0, 1, m).astype(dtype)
+    lib = spmv_hw.load(dtype)
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SPMV_TILE_CLUSTER", mode)
+        y, st = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel="tiles")
+        outs[mode] = (y, st["format"])
+    assert bool(outs["1"][1] & 16) == clustered and not outs["0"][1] & 16
+    assert np.array_equal(outs["1"][0].view(np.uint8), outs["0"][0].view(np.uint8))
+    check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), outs["1"][0], dtype)
 
 
 def test_auto_kernel_choice(torch, monkeypatch):
