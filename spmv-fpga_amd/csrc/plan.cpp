@@ -406,9 +406,11 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     int kernel = requested_kernel();
     if (kernel == -1) {
         // automatic choice: the sweep pays once x outgrows ~half an XCD's L2 and the columns of a
-        // row are scattered (the first two columns of sampled rows lie >= 64 apart). Measured on
-        // power-law matrices with 16 nnz/row (profiles/r01_ab_variants.jsonl): tie at x = 1.6 MB,
-        // sweep 1.2x faster at 2.4 MB, 2.3x at 8 MB, 3.4x at 16 MB, 3.9x at 80 MB.
+        // row are scattered: fewer than 30 % of the consecutive column pairs of sampled rows lie
+        // < 64 apart (random: ~0; 2-D 5-point stencil 0.5, 3-D 7-point 0.33, 27-point 0.69, where
+        // the (clustered) tile layout is as fast or faster). Measured on power-law matrices with
+        // 16 nnz/row (profiles/r01_ab_variants.jsonl): tie at x = 1.6 MB, sweep 1.2x faster at
+        // 2.4 MB, 2.3x at 8 MB, 3.4x at 16 MB, 3.9x at 80 MB.
         kernel = kKernelTiles;
         if (nnz && uint64_t(nr_cols) * sizeof(ValueType) >= (2ull << 20) && nnz >= 16ull * kSweepThreads) {
             SPMV_TRY(hipMalloc(&trp.p, (size_t(nr_rows) + 1) * sizeof(IndexType)));
@@ -416,7 +418,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
                                     hipMemcpyHostToDevice, s));
             if (probe_locality((const IndexType *)trp.p, d_col, nr_rows, s, &p->locality))
                 return 1;
-            if (p->locality < 0.5)
+            if (p->locality < 0.3)
                 kernel = kKernelSweep;
         }
     }
