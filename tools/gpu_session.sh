@@ -29,7 +29,8 @@ for s in $STEPS; do
     bench32) run bench_f32 600 python bench.py --dtype f32 --no-cpu ;;
     banded) run bench_banded 300 python bench.py --workload banded ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
-    calib) run calib 300 tools/hbm_calib ;;
+    calib) [ -x tools/hbm_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/hbm_calib.hip -o tools/hbm_calib
+           run calib 300 tools/hbm_calib ;;
     strong) run strong 600 python tools/strong_slices.py ${STRONG_ARGS:-} ;;
     skew) run skew 600 python tools/skew_probe.py ${SKEW_ARGS:-} ;;
     e2e) run reader 600 python tools/bench_reader.py --dir /tmp --threads 1,8,16
