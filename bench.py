@@ -171,8 +171,13 @@ def cpu_baseline(lib, rp, col, val, x, y_gpu, reps, args_threads=16):
                             "kind": "port", "sample": f"same matrix, row-parallel restatement: {nt} threads "
                                                       f"over nnz-balanced row slices, median of {len(times_mt)} "
                                                       f"runs, {t_mt * 1e3:.1f} ms/SpMV"}
+    yg = y_gpu.cpu().numpy().astype(np.float64)
+    yr = y.astype(np.float64)
+    nz = yr != 0
+    rel = float(np.max(np.abs(yg[nz] - yr[nz]) / np.abs(yr[nz]))) if nz.any() else 0.0
     parity = {"max_scaled_err": err, "tol": 1e-6 if h_val.dtype == np.float64 else 1e-4,
-              "ref_abs_1e-5_errors": abs_errors, "pass": bool(err <= (1e-6 if h_val.dtype == np.float64 else 1e-4))}
+              "max_rel_err": rel, "ref_abs_1e-5_errors": abs_errors,
+              "pass": bool(err <= (1e-6 if h_val.dtype == np.float64 else 1e-4))}
     return base, parity
 
 
