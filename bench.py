@@ -387,6 +387,19 @@ def main():
             torch.cuda.synchronize()
             barrier(world)
             res[f"{mode}_ms"] = round(spmv_dist.max_over_ranks((time.perf_counter() - te0) * 1e3 / reps, dev), 4)
+        # x replication (done once per matrix; the bench generates x on every rank instead)
+        xb = x.clone()
+        spmv_dist.broadcast_x(xb)
+        torch.cuda.synchronize()
+        barrier(world)
+        tb0 = time.perf_counter()
+        for _ in range(3):
+            spmv_dist.broadcast_x(xb)
+        torch.cuda.synchronize()
+        barrier(world)
+        res["x_broadcast_ms"] = round(spmv_dist.max_over_ranks((time.perf_counter() - tb0) * 1e3 / 3, dev), 4)
+        assert torch.equal(xb, x)  # every rank generates the same x
+        del xb
         res["y_bytes"] = n_total * y.element_size()
         res["e2e_gflops_with_gather"] = round(2.0 * nnz_all / ((ms + res["gather_ms"]) * 1e-3) / 1e9, 2)
         exchange = res

@@ -7,7 +7,7 @@ loop csr_hw_wrapper.cpp:276-281). Here a CU is a GPU rank:
 
   * row_slice(): the nnz-balanced contiguous slice of rank r (spmv_partition_rows in the C-ABI,
     S1 rule without the FPGA alignment rules S2/S3);
-  * x is generated/uploaded on every rank (replicated, no collective);
+  * x is replicated: broadcast once from rank 0 (broadcast_x) or generated on every rank;
   * the y merge is a real exchange step, done three ways over RCCL:
       - "reduce": every rank contributes a full-length partial y (zeros outside its slice) to
         an RCCL reduce(SUM) on rank 0 -- the literal accum_results '+=' mapping;
@@ -80,6 +80,15 @@ def exchange_allgather(y_slice: torch.Tensor, counts, out: torch.Tensor | None =
         out[off:off + c].copy_(parts[r, :c])
         off += c
     return out
+
+
+def broadcast_x(x: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """x replicated from rank `src` to every rank (broadcast once, then resident)."""
+    buf = _staged(x)
+    dist.broadcast(buf, src=src)
+    if buf is not x:
+        x.copy_(buf)
+    return x
 
 
 def max_over_ranks(value: float, device) -> float:

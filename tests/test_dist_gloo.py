@@ -57,6 +57,9 @@ def _worker(rank, world, port, mode, q):
         else:  # every rank receives the whole y (next x of an iterative solver)
             full = sdist.exchange_allgather(y_t, sdist.slice_counts(bounds))
             assert np.array_equal(full.numpy(), oracle.spmv_gold(row_ptr, col, val, x))
+        xb = torch.from_numpy(x.copy() if rank == 0 else np.zeros_like(x))
+        sdist.broadcast_x(xb)
+        assert np.array_equal(xb.numpy(), x)
         m = sdist.max_over_ranks(float(rank), torch.device("cpu"))
         if rank == 0:
             y_ref = oracle.spmv_gold(row_ptr, col, val, x)
