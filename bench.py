@@ -317,6 +317,8 @@ def main():
         kname = "k_spmv_sweep_packed" if st["format"] & 2 else "k_spmv_sweep"
     elif st["kernel"] == 1:
         kname = "k_spmv_gold"
+    elif st["kernel"] == 3:
+        kname = "k_spmv_fpga"
     else:
         kname = "k_spmv_tiles"
     traffic = None

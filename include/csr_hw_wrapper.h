@@ -78,9 +78,11 @@ typedef struct spmv_plan_stats {
     uint64_t algorithmic_bytes;  /* compulsory CSR bytes per SpMV, SURVEY.md §8(d) */
     int32_t device;              /* HIP device ordinal */
     int32_t kernel;              /* 0 = flagged-tile gather, 1 = spmv_gold order (bitwise), 2 = panel
-                                    sweep. Chosen automatically, or by env
-                                    SPMV_HW_KERNEL = tiles | gold | sweep | tune (build both
-                                    layouts, time them on the matrix, keep the faster) */
+                                    sweep, 3 = the reference FPGA path's order for env
+                                    SPMV_FPGA_VF / SPMV_FPGA_BLOCK (bitwise).
+                                    Chosen automatically, or by env SPMV_HW_KERNEL = tiles |
+                                    gold | sweep | fpga | tune (build tiles and sweep, time them
+                                    on the matrix, keep the faster) */
     int32_t blocks;              /* column blocks of the representation */
     int32_t format;              /* bit 0: 16- or 8-bit column offsets per tile (kernel 0), bit 3:
                                     8-bit, bit 4: 16-bit (cluster, offset) with 4 bases per tile;

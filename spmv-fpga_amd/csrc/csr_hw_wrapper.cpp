@@ -161,7 +161,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         const spmv_plan &pl = *h->plan;
         const bool sweep = pl.kernel == kKernelSweep;
         // stored entries of the representation (padded for tiles and sweep, plain for gold)
-        const uint64_t stored = sweep ? pl.ent_pad : pl.kernel == kKernelGold ? pl.nnz : pl.nnz_pad;
+        const uint64_t stored = sweep ? pl.ent_pad : pl.kernel != kKernelTiles ? pl.nnz : pl.nnz_pad;
         const uint64_t val_bytes = stored * sizeof(ValueType);
         // the index stream of the unit's representation (opaque device address)
         h->sub[0] = sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)

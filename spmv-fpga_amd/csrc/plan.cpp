@@ -106,6 +106,8 @@ static int requested_kernel()
         return kKernelSweep;
     if (!std::strcmp(e, "gold"))
         return kKernelGold;
+    if (!std::strcmp(e, "fpga"))
+        return kKernelFpga;
     return -1;
 }
 
@@ -287,6 +289,66 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
     return 0;
 }
 
+// FPGA order: VF / block width from the environment (the reference's compile-time VF and
+// COLS_DIV_BLOCKS, util.h:31-59; defaults VF = 1 as its Makefile:16, 32768 columns), and every
+// row's entries stably ordered by column block (the reference walks each block's entries of a
+// row in CSR order, create_block_matrix); rows that are already block-ordered stay as they are.
+static int order_rows_by_block(spmv_plan &p, const IndexType *h_row_ptr, hipStream_t s)
+{
+    if (const char *v = std::getenv("SPMV_FPGA_VF")) {
+        const int vf = std::atoi(v);
+        if (vf != 1 && vf != 2 && vf != 4 && vf != 8) {
+            set_error("SPMV_FPGA_VF must be 1, 2, 4 or 8");
+            return 1;
+        }
+        p.fpga_vf = vf;
+    }
+    if (const char *b = std::getenv("SPMV_FPGA_BLOCK")) {
+        const long w = std::atol(b);
+        if (w < 1 || w > 0x7FFFFFFFL) {
+            set_error("SPMV_FPGA_BLOCK must be a positive column count");
+            return 1;
+        }
+        p.fpga_width = (uint32_t)w;
+    }
+    if (!p.nnz)
+        return 0;
+    std::vector<uint32_t> col(p.nnz);
+    SPMV_TRY(hipMemcpyAsync(col.data(), p.d_col, p.nnz * 4, hipMemcpyDeviceToHost, s));
+    SPMV_TRY(hipStreamSynchronize(s));
+    bool sorted = true;
+    for (IndexType r = 0; r < p.nr_rows && sorted; ++r)
+        for (uint64_t k = uint64_t(h_row_ptr[r]) + 1; k < h_row_ptr[r + 1]; ++k)
+            if (col[k] / p.fpga_width < col[k - 1] / p.fpga_width) {
+                sorted = false;
+                break;
+            }
+    if (sorted)
+        return 0;
+    std::vector<ValueType> val(p.nnz);
+    SPMV_TRY(hipMemcpyAsync(val.data(), p.d_val, p.nnz * sizeof(ValueType), hipMemcpyDeviceToHost, s));
+    SPMV_TRY(hipStreamSynchronize(s));
+    std::vector<uint32_t> idx;
+    std::vector<uint32_t> c2(col);
+    std::vector<ValueType> v2(val);
+    for (IndexType r = 0; r < p.nr_rows; ++r) {
+        const uint64_t b = h_row_ptr[r], e = h_row_ptr[r + 1];
+        idx.resize(e - b);
+        for (uint64_t k = b; k < e; ++k)
+            idx[k - b] = (uint32_t)k;
+        std::stable_sort(idx.begin(), idx.end(),
+                         [&](uint32_t i, uint32_t j) { return col[i] / p.fpga_width < col[j] / p.fpga_width; });
+        for (uint64_t k = b; k < e; ++k) {
+            c2[k] = col[idx[k - b]];
+            v2[k] = val[idx[k - b]];
+        }
+    }
+    SPMV_TRY(hipMemcpyAsync(p.d_col, c2.data(), p.nnz * 4, hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipMemcpyAsync(p.d_val, v2.data(), p.nnz * sizeof(ValueType), hipMemcpyHostToDevice, s));
+    SPMV_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
 // Builds plan P's layout for `kernel` from the validated device CSR and loads its kernels.
 static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexType *h_row_ptr,
                         const IndexType *d_col, const ValueType *d_val, hipStream_t s)
@@ -299,8 +361,10 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
         else if (rc)
             return 1;
     }
-    if (kernel == kKernelGold) {
+    if (kernel == kKernelGold || kernel == kKernelFpga) {
         if (build_gold(P, h_row_ptr, d_col, d_val, s))
+            return 1;
+        if (kernel == kKernelFpga && order_rows_by_block(P, h_row_ptr, s))
             return 1;
     } else if (kernel != kKernelSweep) {
         if (build_tiles(P, h_row_ptr, d_col, d_val, s))
@@ -311,7 +375,7 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
     // failure here only means the first run loads them)
     if (P.kernel == kKernelSweep) {
         (void)launch_sweep(P, nullptr, nullptr, s, true);
-    } else if (P.kernel == kKernelGold) {
+    } else if (P.kernel == kKernelGold || P.kernel == kKernelFpga) {
         (void)launch_gold(P, nullptr, nullptr, s, true);
     } else {
         (void)launch_spmv(P, nullptr, nullptr, s, true);
@@ -457,7 +521,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     } else {
         if (build_layout(*p, kernel, requested_kernel() < 0, h_row_ptr, d_col, d_val, s))
             return 1;
-        trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelGold ? "build gold layout"
+        trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel != kKernelTiles ? "build CSR layout"
                                                                                         : "build tile layout", s);
     }
     *out = p.release();
@@ -488,7 +552,7 @@ spmv_plan::~spmv_plan()
 
 uint64_t spmv_plan::device_bytes() const
 {
-    if (kernel == kKernelGold)
+    if (kernel == kKernelGold || kernel == kKernelFpga)
         return (uint64_t(nr_rows) + 1) * 4 + nnz * (4 + sizeof(ValueType));
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
@@ -577,7 +641,7 @@ static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStrea
         p->ev_used += 2;
         SPMV_TRY(hipEventRecord(e0, s));
     }
-    if (p->kernel == kKernelSweep || p->kernel == kKernelGold) {
+    if (p->kernel != kKernelTiles) {
         SPMV_TRY(p->kernel == kKernelSweep ? launch_sweep(*p, d_x, d_y, s) : launch_gold(*p, d_x, d_y, s));
         if (timing)
             SPMV_TRY(hipEventRecord(e1, s));
@@ -665,9 +729,10 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->nr_nzeros = p->nnz;
     st->nr_nonempty_rows = p->nzr;
     // work units of the main kernel: tiles, sweep units (panel pieces), or long rows (gold)
-    st->nr_tiles = p->kernel == kKernelSweep ? p->nunits : p->kernel == kKernelGold ? p->nlong : p->ntiles;
+    const bool csr = p->kernel == kKernelGold || p->kernel == kKernelFpga;
+    st->nr_tiles = p->kernel == kKernelSweep ? p->nunits : csr ? p->nlong : p->ntiles;
     st->tile_nnz = p->kernel == kKernelSweep ? (p->nunits ? p->ent_pad / p->nunits : 0)
-                   : p->kernel == kKernelGold ? (uint64_t)kGoldLong : kTileNnz;
+                   : csr ? (uint64_t)kGoldLong : kTileNnz;
     st->device_bytes = p->device_bytes();
     st->algorithmic_bytes = p->algorithmic_bytes();
     st->device = p->device;

@@ -45,6 +45,7 @@ constexpr uint64_t kSweepChunk = 128;              // entries per packed chunk (
 constexpr int kKernelTiles = 0;  // flagged-tile wave kernel, x gathered through the caches
 constexpr int kKernelGold = 1;   // spmv_gold's exact order (bitwise reference results)
 constexpr int kKernelSweep = 2;  // panel sweep: y in LDS, columns swept in order (x from L2)
+constexpr int kKernelFpga = 3;   // the reference FPGA path's order for (VF, block width), bitwise
 constexpr int kGoldLong = 128;   // gold plan stats: rows longer than this count as long
 
 }  // namespace spmvhw
@@ -79,6 +80,8 @@ struct spmv_plan {
     // gold-order representation (kernel 1, gold.hip): plain CSR in d_rp / d_col / d_val
     uint32_t *d_rp = nullptr;         // rebased row_ptr[nr_rows + 1]
     uint64_t nlong = 0;               // rows with more than kGoldLong entries (stats)
+    int fpga_vf = 1;                  // kernel 3: vectorisation factor (env SPMV_FPGA_VF)
+    uint32_t fpga_width = 32768;      // kernel 3: column-block width (env SPMV_FPGA_BLOCK)
 
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;

@@ -509,6 +509,102 @@ def test_gold_kernel_through_reference_api_is_bitwise(torch, monkeypatch, units)
         _bitwise(y, y_gold)
 
 
+# ---- FPGA order: bitwise the reference hardware path's sums (spmv.cpp:66-104,
+#      csr_hw.cpp:209-243 + 1543-1562) for a VF / column-block width ----
+KERNEL_ID["fpga"] = 3
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("dtype,tag", DTYPES)
+@pytest.mark.parametrize("vf", [1, 2, 4, 8])
+@pytest.mark.parametrize("block", [32768, 700])
+def test_fpga_order_bitwise_equals_oracle_fixture(torch, monkeypatch, name, dtype, tag, vf, block):
+    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+    monkeypatch.setenv("SPMV_FPGA_VF", str(vf))
+    monkeypatch.setenv("SPMV_FPGA_BLOCK", str(block))
+    lib = spmv_hw.load(dtype)
+    path = os.path.join(GOLDEN, manifest()[name]["file"])
+    _, c, row_ptr, col, val, _ = oracle.read_csr(path, dtype)
+    x, y_gold = golden_arrays(name, tag)
+    y, _ = run_device(torch, lib, row_ptr, col, val, x, c, expect_kernel="fpga")
+    _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, c, block, vf))
+    check(row_ptr, col, val, x, y_gold, y, dtype)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("vf,block", [(1, 32768), (4, 65536), (8, 4096)])
+def test_fpga_order_bitwise_synthetic(torch, monkeypatch, dtype, vf, block):
+    """1M-row power-law matrix (rows up to ~20K entries, many blocks per row)."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+    monkeypatch.setenv("SPMV_FPGA_VF", str(vf))
+    monkeypatch.setenv("SPMV_FPGA_BLOCK", str(block))
+    lib = spmv_hw.load(dtype)
+    n = 1_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 16 * n, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    assert plan.stats()["kernel"] == 3
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    h = [t.cpu().numpy() for t in (rp, col, val, x, y)]
+    row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
+    _bitwise(yy, oracle.spmv_fpga_order(row_ptr, c, v, xx, n, block, vf))
+    plan.destroy()
+
+
+@pytest.mark.parametrize("vf", [2, 8])
+def test_fpga_order_unsorted_rows(torch, monkeypatch, vf):
+    """Rows whose columns are not ordered: the plan stably groups each row's entries by column
+    block (as create_block_matrix visits them), keeping the CSR order within a block."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+    monkeypatch.setenv("SPMV_FPGA_VF", str(vf))
+    monkeypatch.setenv("SPMV_FPGA_BLOCK", "97")
+    rng = np.random.default_rng(21)
+    n, m = 5000, 1000
+    row_ptr, col, val, x = random_csr(rng, n, m, rng.integers(0, 70, n), np.float64)
+    for i in range(n):  # shuffle every row
+        rng.shuffle(col[row_ptr[i]:row_ptr[i + 1]])
+    lib = spmv_hw.load(np.float64)
+    y, _ = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel="fpga")
+    _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, m, 97, vf))
+
+
+def test_fpga_order_env_errors(torch, monkeypatch):
+    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+    lib = spmv_hw.load(np.float64)
+    row_ptr = np.array([0, 1], np.uint32)
+    for var, bad in (("SPMV_FPGA_VF", "3"), ("SPMV_FPGA_BLOCK", "0")):
+        with monkeypatch.context() as mp:
+            mp.setenv(var, bad)
+            with pytest.raises(RuntimeError, match=var):
+                run_device(torch, lib, row_ptr, np.zeros(1, np.uint32), np.ones(1), np.ones(1), 1)
+
+
+@pytest.mark.parametrize("units", [1, 3])
+def test_fpga_order_through_reference_api(torch, monkeypatch, units):
+    """main.cpp's flow (y_fpga zeroed, then spmv_hw) with SPMV_HW_KERNEL=fpga and the block
+    width of read_csr_header: y equals the restated FPGA arithmetic bit for bit."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+    monkeypatch.setenv("SPMV_FPGA_VF", "4")
+    monkeypatch.setenv("SPMV_NGPUS", str(units))
+    lib = spmv_hw.load(np.float64)
+    for name in FIXTURES:
+        path = os.path.join(GOLDEN, manifest()[name]["file"])
+        n, c, row_ptr, col, val, _ = oracle.read_csr(path, np.float64)
+        x, _ = golden_arrays(name, "f64")
+        m = lib.make_csr_matrix(row_ptr, col, val, c)
+        hw, bm = lib.create_csr_hw_matrix(m)
+        hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(x), hw[0].contents.blocks, hw[0].contents.nr_cols)
+        y_vec = lib.make_csr_vector(np.zeros(n))
+        lib.spmv_hw(hw, hx, y_vec, bm)
+        y = np.ctypeslib.as_array(y_vec.values, (n,)).copy()
+        lib.delete_csr_hw_matrix(hw)
+        lib.free_bitmap(bm)
+        lib.delete_csr_hw_x_vector(hx)
+        _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, c, 32768, 4))
+
+
 @pytest.mark.parametrize("kern", ["sweep", "tiles", "gold"])
 def test_dense_rows_among_short_ones(torch, monkeypatch, kern):
     """Ragged extreme: two rows of 600K entries among 400K rows of ~16. The sweep cuts the
