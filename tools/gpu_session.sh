@@ -22,8 +22,8 @@ run() {  # name seconds cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf -x ;;
-    tests_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    tests_all) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench32) run bench_f32 600 python bench.py --dtype f32 --no-cpu ;;
