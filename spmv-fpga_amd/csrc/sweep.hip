@@ -196,7 +196,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
 // LAG = 0: one workgroup barrier per iteration. LAG = k > 0: no barrier; each wave publishes
 // its iteration count in LDS and only waits (s_sleep) while it is more than k iterations
 // ahead of the slowest wave, so the vector-memory pipe never drains at a common barrier.
-template <typename V, int T, int Q, bool NT, int LAG = 0>
+template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
@@ -233,6 +233,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
             uint64_t wbase = base + q * kGroup + 128ull * wave;  // this wave's chunk
             ok[q] = wbase < e1;                                   // wave-uniform
             wbase = ok[q] ? wbase : last_chunk;
+            if constexpr (ABL == 3 || ABL == 4)  // ablation: entries re-read from the unit's first 4K (L2-resident)
+                wbase = e0 + ((wbase - e0) & 4095u);
             const uint64_t e = wbase + lane2;
             w[q] = lds_<NT>(reinterpret_cast<const u32x2 *>(rc + e));
             cb[q] = cbase[wbase >> 7];
@@ -241,8 +243,22 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         V xv[Q][2];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            xv[q][0] = x[cb[q] + (w[q].x & 0xFFFFu)];
-            xv[q][1] = x[cb[q] + (w[q].y & 0xFFFFu)];
+            // ABL (measurement-only ablations, variants 60/61): 1 = x index folded into a 256 KiB
+            // window (every gather an L2 hit, same request count), 2 = no gathers
+            if constexpr (ABL == 2 || ABL == 5) {
+                xv[q][0] = V(w[q].x & 1u);
+                xv[q][1] = V(w[q].y & 1u);
+            } else if constexpr (ABL == 6) {  // x gathers non-temporal (nt)
+                xv[q][0] = __builtin_nontemporal_load(x + cb[q] + (w[q].x & 0xFFFFu));
+                xv[q][1] = __builtin_nontemporal_load(x + cb[q] + (w[q].y & 0xFFFFu));
+            } else if constexpr (ABL == 7) {  // x gathers L1-bypassing (sc1)
+                xv[q][0] = __hip_atomic_load(x + cb[q] + (w[q].x & 0xFFFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                xv[q][1] = __hip_atomic_load(x + cb[q] + (w[q].y & 0xFFFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                const uint32_t m = (ABL == 1 || ABL == 4) ? 0x7FFFu : 0xFFFFFFFFu;
+                xv[q][0] = x[(cb[q] + (w[q].x & 0xFFFFu)) & m];
+                xv[q][1] = x[(cb[q] + (w[q].y & 0xFFFFu)) & m];
+            }
         }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -429,8 +445,8 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>, grid, block, lds, s, p.d_s_col,   \
                        p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
     if (p.sweep_packed) {
-#define PK(Q, LAG)                                                                                  \
-    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, true, LAG>, grid, block, lds, s, p.d_s_col, \
+#define PK(Q, LAG, ...)                                                                             \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, true, LAG __VA_OPT__(,) __VA_ARGS__>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
@@ -445,6 +461,13 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 32: PK(1, 2); break;
         case 33: PK(1, 4); break;
         case 34: PK(2, 3); break;
+        case 60: if (p.nr_cols >= 32768) { PK(2, 2, 1); } else { PK(2, 2); } break;  // ablation: x gathers all L2 hits (wrong y; measurement only)
+        case 61: PK(2, 2, 2); break;  // ablation: no x gathers (wrong y; measurement only)
+        case 62: PK(2, 2, 3); break;  // ablation: entries from L2 (first 16K of the unit), real gathers
+        case 63: if (p.nr_cols >= 32768) { PK(2, 2, 4); } else { PK(2, 2); } break;  // entries + x from L2
+        case 59: PK(2, 1000); break;  // no wave sync (lag never reached)
+        case 57: PK(2, 2, 6); break;  // x gathers with the nt bit
+        case 58: PK(2, 2, 7); break;  // x gathers that bypass L1 (sc1)
         default: PK(2, 2); break;
         }
 #undef PK
