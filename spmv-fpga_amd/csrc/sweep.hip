@@ -217,6 +217,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         progress[threadIdx.x] = 0;
     __syncthreads();
     uint32_t iter = 0;
+    SweepAcc sink = 0;  // ablations 8/9 only
     constexpr uint64_t kGroup = 2ull * T;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane2 = 2u * (threadIdx.x & 63);
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
             uint64_t wbase = base + q * kGroup + 128ull * wave;  // this wave's chunk
             ok[q] = wbase < e1;                                   // wave-uniform
             wbase = ok[q] ? wbase : last_chunk;
-            if constexpr (ABL == 3 || ABL == 4)  // ablation: entries re-read from the unit's first 4K (L2-resident)
+            if constexpr (ABL == 3 || ABL == 4 || ABL == 9)  // ablation: entries re-read from the unit's first 4K (L2-resident)
                 wbase = e0 + ((wbase - e0) & 4095u);
             const uint64_t e = wbase + lane2;
             w[q] = lds_<NT>(reinterpret_cast<const u32x2 *>(rc + e));
@@ -255,15 +256,19 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
                 xv[q][0] = __hip_atomic_load(x + cb[q] + (w[q].x & 0xFFFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 xv[q][1] = __hip_atomic_load(x + cb[q] + (w[q].y & 0xFFFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
-                const uint32_t m = (ABL == 1 || ABL == 4) ? 0x7FFFu : 0xFFFFFFFFu;
+                const uint32_t m = (ABL == 1 || ABL == 4 || ABL == 9) ? 0x7FFFu : 0xFFFFFFFFu;
                 xv[q][0] = x[(cb[q] + (w[q].x & 0xFFFFu)) & m];
                 xv[q][1] = x[(cb[q] + (w[q].y & 0xFFFFu)) & m];
             }
         }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            atomicAdd(&ylds[ok[q] ? (w[q].x >> 16) : R], SweepAcc(v[q][0]) * SweepAcc(xv[q][0]));
-            atomicAdd(&ylds[ok[q] ? (w[q].y >> 16) : R], SweepAcc(v[q][1]) * SweepAcc(xv[q][1]));
+            if constexpr (ABL == 8 || ABL == 9) {  // ablation: no LDS adds (register sum)
+                sink += SweepAcc(v[q][0]) * SweepAcc(xv[q][0]) + SweepAcc(v[q][1]) * SweepAcc(xv[q][1]);
+            } else {
+                atomicAdd(&ylds[ok[q] ? (w[q].x >> 16) : R], SweepAcc(v[q][0]) * SweepAcc(xv[q][0]));
+                atomicAdd(&ylds[ok[q] ? (w[q].y >> 16) : R], SweepAcc(v[q][1]) * SweepAcc(xv[q][1]));
+            }
         }
         if constexpr (LAG == 0) {
             __syncthreads();
@@ -288,6 +293,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
             }
         }
     }
+    if constexpr (ABL == 8 || ABL == 9)
+        atomicAdd(&ylds[R], sink);
     __syncthreads();
     write_panel<V, T>(ylds, R, y + r0, pieces, part, stride);
 }
@@ -445,9 +452,10 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>, grid, block, lds, s, p.d_s_col,   \
                        p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
     if (p.sweep_packed) {
-#define PK(Q, LAG, ...)                                                                             \
-    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, true, LAG __VA_OPT__(,) __VA_ARGS__>, grid, block, lds, s, p.d_s_col, \
+#define PKN(NT, Q, LAG, ...)                                                                        \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG __VA_OPT__(,) __VA_ARGS__>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
+#define PK(Q, LAG, ...) PKN(true, Q, LAG __VA_OPT__(,) __VA_ARGS__)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
         case 15: PK(2, 0); break;
@@ -463,14 +471,18 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 34: PK(2, 3); break;
         case 60: if (p.nr_cols >= 32768) { PK(2, 2, 1); } else { PK(2, 2); } break;  // ablation: x gathers all L2 hits (wrong y; measurement only)
         case 61: PK(2, 2, 2); break;  // ablation: no x gathers (wrong y; measurement only)
-        case 62: PK(2, 2, 3); break;  // ablation: entries from L2 (first 16K of the unit), real gathers
+        case 62: PK(2, 2, 3); break;  // ablation: entries from L2 (first 4K of the unit), real gathers
         case 63: if (p.nr_cols >= 32768) { PK(2, 2, 4); } else { PK(2, 2); } break;  // entries + x from L2
         case 59: PK(2, 1000); break;  // no wave sync (lag never reached)
+        case 56: PKN(false, 2, 2); break;  // plain (temporal) entry loads
+        case 54: PK(2, 2, 8); break;  // ablation: no LDS adds
+        case 55: if (p.nr_cols >= 32768) { PK(2, 2, 9); } else { PK(2, 2); } break;  // no LDS adds, all L2
         case 57: PK(2, 2, 6); break;  // x gathers with the nt bit
         case 58: PK(2, 2, 7); break;  // x gathers that bypass L1 (sc1)
         default: PK(2, 2); break;
         }
 #undef PK
+#undef PKN
         return;
     }
     switch (p.sweep_variant) {

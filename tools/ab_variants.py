@@ -116,7 +116,7 @@ def main():
                 torch.cuda.synchronize()
                 if ref is None:
                     ref = y.clone()
-                elif int(var) < 60:  # 60+: measurement-only ablations (wrong y by design)
+                elif int(var) not in (54, 55, 60, 61, 62, 63):  # measurement-only ablations (wrong y)
                     err = float(((ref - y).abs().max() / ref.abs().max().clamp_min(1e-300)).item())
                     assert err < (1e-9 if a.dtype == "f64" else 1e-5), f"{v} changed the result ({err})"
                 plan.set_timing(True)
