@@ -108,6 +108,8 @@ static int requested_kernel()
         return kKernelGold;
     if (!std::strcmp(e, "fpga"))
         return kKernelFpga;
+    if (!std::strcmp(e, "blocked"))
+        return kKernelBlocked;
     return -1;
 }
 
@@ -293,7 +295,7 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
 // COLS_DIV_BLOCKS, util.h:31-59; defaults VF = 1 as its Makefile:16, 32768 columns), and every
 // row's entries stably ordered by column block (the reference walks each block's entries of a
 // row in CSR order, create_block_matrix); rows that are already block-ordered stay as they are.
-static int order_rows_by_block(spmv_plan &p, const IndexType *h_row_ptr, hipStream_t s)
+static int fpga_params(spmv_plan &p)
 {
     if (const char *v = std::getenv("SPMV_FPGA_VF")) {
         const int vf = std::atoi(v);
@@ -311,6 +313,13 @@ static int order_rows_by_block(spmv_plan &p, const IndexType *h_row_ptr, hipStre
         }
         p.fpga_width = (uint32_t)w;
     }
+    return 0;
+}
+
+static int order_rows_by_block(spmv_plan &p, const IndexType *h_row_ptr, hipStream_t s)
+{
+    if (fpga_params(p))
+        return 1;
     if (!p.nnz)
         return 0;
     std::vector<uint32_t> col(p.nnz);
@@ -361,7 +370,10 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
         else if (rc)
             return 1;
     }
-    if (kernel == kKernelGold || kernel == kKernelFpga) {
+    if (kernel == kKernelBlocked) {
+        if (fpga_params(P) || build_blocked(P, h_row_ptr, d_col, d_val, s))
+            return 1;
+    } else if (kernel == kKernelGold || kernel == kKernelFpga) {
         if (build_gold(P, h_row_ptr, d_col, d_val, s))
             return 1;
         if (kernel == kKernelFpga && order_rows_by_block(P, h_row_ptr, s))
@@ -375,6 +387,8 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
     // failure here only means the first run loads them)
     if (P.kernel == kKernelSweep) {
         (void)launch_sweep(P, nullptr, nullptr, s, true);
+    } else if (P.kernel == kKernelBlocked) {
+        (void)launch_blocked(P, nullptr, nullptr, s, true);
     } else if (P.kernel == kKernelGold || P.kernel == kKernelFpga) {
         (void)launch_gold(P, nullptr, nullptr, s, true);
     } else {
@@ -539,7 +553,8 @@ spmv_plan::~spmv_plan()
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
                       (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
-                      (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase})
+                      (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
+                      (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -554,6 +569,9 @@ uint64_t spmv_plan::device_bytes() const
 {
     if (kernel == kKernelGold || kernel == kKernelFpga)
         return (uint64_t(nr_rows) + 1) * 4 + nnz * (4 + sizeof(ValueType));
+    if (kernel == kKernelBlocked)  // entries, kptr, kpos, rl, partials, rp2, chunks, units
+        return nnz * (2 + sizeof(ValueType)) + (nkpairs + 1) * 4 + nkpairs * (4 + 2 + sizeof(ValueType)) +
+               (uint64_t(nr_rows) + 1) * 4 + (nchunks + 1) * 4 + nunits * 8 + 4;
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
@@ -642,7 +660,9 @@ static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStrea
         SPMV_TRY(hipEventRecord(e0, s));
     }
     if (p->kernel != kKernelTiles) {
-        SPMV_TRY(p->kernel == kKernelSweep ? launch_sweep(*p, d_x, d_y, s) : launch_gold(*p, d_x, d_y, s));
+        SPMV_TRY(p->kernel == kKernelSweep     ? launch_sweep(*p, d_x, d_y, s)
+                 : p->kernel == kKernelBlocked ? launch_blocked(*p, d_x, d_y, s)
+                                               : launch_gold(*p, d_x, d_y, s));
         if (timing)
             SPMV_TRY(hipEventRecord(e1, s));
         return 0;
@@ -730,14 +750,16 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->nr_nonempty_rows = p->nzr;
     // work units of the main kernel: tiles, sweep units (panel pieces), or long rows (gold)
     const bool csr = p->kernel == kKernelGold || p->kernel == kKernelFpga;
-    st->nr_tiles = p->kernel == kKernelSweep ? p->nunits : csr ? p->nlong : p->ntiles;
-    st->tile_nnz = p->kernel == kKernelSweep ? (p->nunits ? p->ent_pad / p->nunits : 0)
-                   : csr ? (uint64_t)kGoldLong : kTileNnz;
+    st->nr_tiles = (p->kernel == kKernelSweep || p->kernel == kKernelBlocked) ? p->nunits : csr ? p->nlong : p->ntiles;
+    st->tile_nnz = p->kernel == kKernelSweep     ? (p->nunits ? p->ent_pad / p->nunits : 0)
+                   : p->kernel == kKernelBlocked ? (p->nunits ? p->nnz / p->nunits : 0)
+                   : csr                         ? (uint64_t)kGoldLong
+                                                 : kTileNnz;
     st->device_bytes = p->device_bytes();
     st->algorithmic_bytes = p->algorithmic_bytes();
     st->device = p->device;
     st->kernel = p->kernel;
-    st->blocks = 1;
+    st->blocks = p->kernel == kKernelBlocked ? (uint32_t)((uint64_t(p->nr_cols) + p->fpga_width - 1) / p->fpga_width) : 1;
     st->format = (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) |
                  (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0);
     return 0;

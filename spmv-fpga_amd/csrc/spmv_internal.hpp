@@ -46,6 +46,8 @@ constexpr int kKernelTiles = 0;  // flagged-tile wave kernel, x gathered through
 constexpr int kKernelGold = 1;   // spmv_gold's exact order (bitwise reference results)
 constexpr int kKernelSweep = 2;  // panel sweep: y in LDS, columns swept in order (x from L2)
 constexpr int kKernelFpga = 3;   // the reference FPGA path's order for (VF, block width), bitwise
+constexpr int kKernelBlocked = 4;  // the same order by the reference's dataflow: x blocks in LDS,
+                                   // per-block partials, block-ordered merge (blocked.hip)
 constexpr int kGoldLong = 128;   // gold plan stats: rows longer than this count as long
 
 }  // namespace spmvhw
@@ -82,6 +84,18 @@ struct spmv_plan {
     uint64_t nlong = 0;               // rows with more than kGoldLong entries (stats)
     int fpga_vf = 1;                  // kernel 3: vectorisation factor (env SPMV_FPGA_VF)
     uint32_t fpga_width = 32768;      // kernel 3: column-block width (env SPMV_FPGA_BLOCK)
+
+    // blocked representation (kernel 4, blocked.hip): entries by (block, row) in d_val (values)
+    // and d_colnar (u16 block-relative columns); units in d_unit_panel (block) / d_unit_ent
+    // (compact-row ranges)
+    uint32_t *d_kptr = nullptr;       // first entry of each compact row [nkpairs + 1]
+    uint32_t *d_kpos = nullptr;       // partial slot of each compact row
+    uint32_t *d_rp2 = nullptr;        // row-major offsets of each row's partials [nr_rows + 1]
+    uint16_t *d_rl = nullptr;         // row-major: chunk-local slot of each partial
+    uint32_t *d_chunk_row = nullptr;  // row ranges of the merge chunks [nchunks + 1]
+    ValueType *d_bpart = nullptr;     // block partials (scratch)
+    uint64_t nkpairs = 0, nchunks = 0;
+    bool blocked_xlds = false;        // x block staged in LDS (W * sizeof(V) <= 128 KiB)
 
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
@@ -160,6 +174,11 @@ hipError_t launch_narrow(const uint32_t *d_col, uint64_t nnz, uint64_t nnz_pad, 
 
 // gold.hip
 hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
+
+// blocked.hip
+hipError_t launch_blocked(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
+int build_blocked(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
+                  hipStream_t s);
 
 // sweep.hip
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);

@@ -27,13 +27,14 @@ def torch():
     return t
 
 
-KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "gold"]
-KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "gold": 1}
+KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "gold", "blocked"]
+KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "gold": 1, "blocked": 4}
 
 
 @pytest.fixture(params=KERNELS)
 def kernel(request, monkeypatch):
-    """Plans are built with SPMV_HW_KERNEL forced to each kernel in turn; "tiles_wide" is the
+    """Plans are built with SPMV_HW_KERNEL forced to each kernel in turn ("blocked" with its
+    defaults VF = 1, 32768-column blocks); "tiles_wide" is the
     tile kernel with 32-bit columns (SPMV_TILE_NARROW=0) instead of per-tile offsets and
     "sweep_unpacked" the sweep on 14-byte entries (SPMV_SWEEP_PACKED=0), the layout used when a
     chunk of a panel spans >= 65536 columns."""
@@ -251,7 +252,7 @@ def test_deterministic(torch, kernel, dtype):
     lib = spmv_hw.load(dtype)
     y1, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
     y2, _ = run_device(torch, lib, row_ptr, col, val, x, 30000)
-    if kernel.startswith("tiles") or kernel == "gold":
+    if kernel.startswith("tiles") or kernel in ("gold", "blocked"):
         assert np.array_equal(y1.view(np.uint8), y2.view(np.uint8))
     else:
         assert oracle.scaled_error(row_ptr, col, val, x, y1, y2) <= TIGHT[np.dtype(dtype)]
@@ -511,31 +512,38 @@ def test_gold_kernel_through_reference_api_is_bitwise(torch, monkeypatch, units)
 
 # ---- FPGA order: bitwise the reference hardware path's sums (spmv.cpp:66-104,
 #      csr_hw.cpp:209-243 + 1543-1562) for a VF / column-block width ----
+#      kernel 3 ("fpga": CSR, one in-order pass per row) and kernel 4 ("blocked": the reference's
+#      dataflow, x blocks in LDS, per-block partials, block-ordered merge) ----
 KERNEL_ID["fpga"] = 3
+FPGA_KERNELS = ["fpga", "blocked"]
 
 
 @pytest.mark.parametrize("name", FIXTURES)
 @pytest.mark.parametrize("dtype,tag", DTYPES)
 @pytest.mark.parametrize("vf", [1, 2, 4, 8])
 @pytest.mark.parametrize("block", [32768, 700])
-def test_fpga_order_bitwise_equals_oracle_fixture(torch, monkeypatch, name, dtype, tag, vf, block):
-    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+@pytest.mark.parametrize("kern", FPGA_KERNELS)
+def test_fpga_order_bitwise_equals_oracle_fixture(torch, monkeypatch, name, dtype, tag, vf, block, kern):
+    monkeypatch.setenv("SPMV_HW_KERNEL", kern)
     monkeypatch.setenv("SPMV_FPGA_VF", str(vf))
     monkeypatch.setenv("SPMV_FPGA_BLOCK", str(block))
     lib = spmv_hw.load(dtype)
     path = os.path.join(GOLDEN, manifest()[name]["file"])
     _, c, row_ptr, col, val, _ = oracle.read_csr(path, dtype)
     x, y_gold = golden_arrays(name, tag)
-    y, _ = run_device(torch, lib, row_ptr, col, val, x, c, expect_kernel="fpga")
+    y, _ = run_device(torch, lib, row_ptr, col, val, x, c, expect_kernel=kern)
     _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, c, block, vf))
     check(row_ptr, col, val, x, y_gold, y, dtype)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("vf,block", [(1, 32768), (4, 65536), (8, 4096)])
-def test_fpga_order_bitwise_synthetic(torch, monkeypatch, dtype, vf, block):
-    """1M-row power-law matrix (rows up to ~20K entries, many blocks per row)."""
-    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+@pytest.mark.parametrize("vf,block", [(1, 32768), (4, 65536), (8, 4096), (2, 16384)])
+@pytest.mark.parametrize("kern", FPGA_KERNELS)
+def test_fpga_order_bitwise_synthetic(torch, monkeypatch, dtype, vf, block, kern):
+    """1M-row power-law matrix (rows up to ~20K entries, many blocks per row). For the blocked
+    kernel the x block sits in LDS when it fits 128 KiB (fp32 up to 32768 columns, fp64 up to
+    16384) and is read from L2 otherwise: both forms are covered."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", kern)
     monkeypatch.setenv("SPMV_FPGA_VF", str(vf))
     monkeypatch.setenv("SPMV_FPGA_BLOCK", str(block))
     lib = spmv_hw.load(dtype)
@@ -543,21 +551,25 @@ def test_fpga_order_bitwise_synthetic(torch, monkeypatch, dtype, vf, block):
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 16 * n, seed=4)
     x = spmv_hw.gen_vector(lib, n, seed=6)
     plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
-    assert plan.stats()["kernel"] == 3
+    assert plan.stats()["kernel"] == KERNEL_ID[kern]
     y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
     plan.run(x, y)
     torch.cuda.synchronize()
     h = [t.cpu().numpy() for t in (rp, col, val, x, y)]
     row_ptr, c, v, xx, yy = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3], h[4]
     _bitwise(yy, oracle.spmv_fpga_order(row_ptr, c, v, xx, n, block, vf))
+    plan.run(x, y)  # partials are scratch: a second run gives the same y
+    torch.cuda.synchronize()
+    _bitwise(y.cpu().numpy(), oracle.spmv_fpga_order(row_ptr, c, v, xx, n, block, vf))
     plan.destroy()
 
 
 @pytest.mark.parametrize("vf", [2, 8])
-def test_fpga_order_unsorted_rows(torch, monkeypatch, vf):
+@pytest.mark.parametrize("kern", FPGA_KERNELS)
+def test_fpga_order_unsorted_rows(torch, monkeypatch, vf, kern):
     """Rows whose columns are not ordered: the plan stably groups each row's entries by column
     block (as create_block_matrix visits them), keeping the CSR order within a block."""
-    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+    monkeypatch.setenv("SPMV_HW_KERNEL", kern)
     monkeypatch.setenv("SPMV_FPGA_VF", str(vf))
     monkeypatch.setenv("SPMV_FPGA_BLOCK", "97")
     rng = np.random.default_rng(21)
@@ -566,12 +578,13 @@ def test_fpga_order_unsorted_rows(torch, monkeypatch, vf):
     for i in range(n):  # shuffle every row
         rng.shuffle(col[row_ptr[i]:row_ptr[i + 1]])
     lib = spmv_hw.load(np.float64)
-    y, _ = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel="fpga")
+    y, _ = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel=kern)
     _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, m, 97, vf))
 
 
-def test_fpga_order_env_errors(torch, monkeypatch):
-    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+@pytest.mark.parametrize("kern", FPGA_KERNELS)
+def test_fpga_order_env_errors(torch, monkeypatch, kern):
+    monkeypatch.setenv("SPMV_HW_KERNEL", kern)
     lib = spmv_hw.load(np.float64)
     row_ptr = np.array([0, 1], np.uint32)
     for var, bad in (("SPMV_FPGA_VF", "3"), ("SPMV_FPGA_BLOCK", "0")):
@@ -581,11 +594,21 @@ def test_fpga_order_env_errors(torch, monkeypatch):
                 run_device(torch, lib, row_ptr, np.zeros(1, np.uint32), np.ones(1), np.ones(1), 1)
 
 
+def test_blocked_rejects_blocks_wider_than_16_bit_offsets(torch, monkeypatch):
+    monkeypatch.setenv("SPMV_HW_KERNEL", "blocked")
+    monkeypatch.setenv("SPMV_FPGA_BLOCK", "65537")
+    lib = spmv_hw.load(np.float64)
+    row_ptr = np.array([0, 1], np.uint32)
+    with pytest.raises(RuntimeError, match="16-bit"):
+        run_device(torch, lib, row_ptr, np.zeros(1, np.uint32), np.ones(1), np.ones(1), 1)
+
+
 @pytest.mark.parametrize("units", [1, 3])
-def test_fpga_order_through_reference_api(torch, monkeypatch, units):
-    """main.cpp's flow (y_fpga zeroed, then spmv_hw) with SPMV_HW_KERNEL=fpga and the block
-    width of read_csr_header: y equals the restated FPGA arithmetic bit for bit."""
-    monkeypatch.setenv("SPMV_HW_KERNEL", "fpga")
+@pytest.mark.parametrize("kern", FPGA_KERNELS)
+def test_fpga_order_through_reference_api(torch, monkeypatch, units, kern):
+    """main.cpp's flow (y_fpga zeroed, then spmv_hw) with SPMV_HW_KERNEL=fpga|blocked and the
+    block width of read_csr_header: y equals the restated FPGA arithmetic bit for bit."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", kern)
     monkeypatch.setenv("SPMV_FPGA_VF", "4")
     monkeypatch.setenv("SPMV_NGPUS", str(units))
     lib = spmv_hw.load(np.float64)

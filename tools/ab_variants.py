@@ -91,6 +91,9 @@ def main():
                 if kern.endswith("L"):  # packed, without the lane-order permutation
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_LANE_ORDER"] = "0"
+                if kern.startswith("blocked") and kern[7:].isdigit():  # blockedW: W-column blocks
+                    os.environ["SPMV_FPGA_BLOCK"] = kern[7:]
+                    kern = "blocked"
                 os.environ["SPMV_HW_KERNEL"] = kern
                 if threads:
                     os.environ["SPMV_SWEEP_THREADS"] = threads
@@ -101,6 +104,7 @@ def main():
                 os.environ.pop("SPMV_TILE_NARROW", None)
                 os.environ.pop("SPMV_SWEEP_SPLIT", None)
                 os.environ.pop("SPMV_TILE_XCD", None)
+                os.environ.pop("SPMV_FPGA_BLOCK", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
@@ -116,7 +120,7 @@ def main():
                 torch.cuda.synchronize()
                 if ref is None:
                     ref = y.clone()
-                elif int(var) not in (54, 55, 60, 61, 62, 63):  # measurement-only ablations (wrong y)
+                elif int(var) not in (54, 55, 60, 61, 62, 63) and not (k.startswith("blocked") and var == "1"):  # measurement-only ablations (wrong y)
                     err = float(((ref - y).abs().max() / ref.abs().max().clamp_min(1e-300)).item())
                     assert err < (1e-9 if a.dtype == "f64" else 1e-5), f"{v} changed the result ({err})"
                 plan.set_timing(True)
