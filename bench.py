@@ -2,8 +2,9 @@
 """SpMV benchmark on MI355X — BASELINE.json metric "SpMV GFLOP/s + effective HBM GB/s
 (% roofline), fp64, 1/2/4/8 MI355X".
 
-A step = one y = A*x over the workload's matrix, through the C-ABI plan (spmv_plan_run: the
-flagged-tile kernel + its fix-up), with A, x and y resident in HBM before the timed region.
+A step = one y = A*x over the workload's matrix, through the C-ABI plan (spmv_plan_run with the
+automatically chosen kernel: the panel sweep for the power-law matrix, the flagged tiles for the
+banded one), with A, x and y resident in HBM before the timed region.
 
 Workloads:
   powerlaw (default, config 3): n = m = 10,000,000, nnz = 160,000,000, Pareto(2) row lengths
@@ -21,7 +22,10 @@ Multi-GPU (--gpus N, one process per GPU, torch.distributed over RCCL):
 Extra JSON fields: roofline (dominant kernel of the plan: k_spmv_sweep_packed for the power-law
 matrix, k_spmv_tiles for the banded one; HIP events on its launch stream),
 cpu_baseline (the oracle's restatement of spmv_gold, 1 thread, on the host of the GPU box),
-parity (full-size componentwise-scaled error vs that oracle run).
+parity (full-size componentwise-scaled error vs that oracle run),
+lds_xtiles (power-law, 1 GPU: the same matrix through kernel 4, the reference's dataflow with a
+block of x in LDS per workgroup -- the technique BASELINE configs 3/5 name -- timed beside the
+headline kernel).
 """
 from __future__ import annotations
 
@@ -56,6 +60,8 @@ def parse():
     ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
+    ap.add_argument("--no-xtiles", action="store_true",
+                    help="skip the LDS x-tile (kernel 4, blocked) measurement beside the headline")
     ap.add_argument("--no-strong-companion", action="store_true",
                     help="N > 1 weak runs: skip the config-4 strong-scaling companion measurement")
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -181,6 +187,47 @@ def cpu_baseline(lib, rp, col, val, x, y_gpu, reps, args_threads=16):
     return base, parity
 
 
+def lds_xtiles(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
+    """BASELINE configs 3/5 name LDS-staged x tiles with the reference's 2-D column blocking: the
+    same matrix through kernel 4 (blocked.hip: a block of x in LDS per workgroup, per-block
+    partials, block-ordered merge; VF = 1; blocks of 32768 fp32 / 16384 fp64 columns = 128 KiB
+    of LDS), timed like the headline (HIP events over K launches) and checked against the
+    headline's y. Reported beside `value`, which stays the automatic (fastest) kernel."""
+    saved = {k: os.environ.get(k) for k in ("SPMV_HW_KERNEL", "SPMV_FPGA_BLOCK", "SPMV_FPGA_VF")}
+    os.environ.update({"SPMV_HW_KERNEL": "blocked", "SPMV_FPGA_VF": "1",
+                       "SPMV_FPGA_BLOCK": "32768" if args.dtype == "f32" else "16384"})
+    try:
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, ncols, device=dev_index, stream=stream)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    st = plan.stats()
+    y = torch.empty_like(y_ref)
+    for _ in range(args.warmup):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    for _ in range(args.steps):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    ms, _, launches = plan.timing()
+    plan.set_timing(False)
+    diff = float(((y.double() - y_ref.double()).abs().max() / y_ref.double().abs().max().clamp_min(1e-300)).item())
+    res = {"kernel": "k_blocked_partials + k_blocked_merge",
+           "block_columns": 32768 if args.dtype == "f32" else 16384, "blocks": st["blocks"], "units": st["nr_tiles"],
+           "ms_per_step": round(ms, 5), "launches": launches,
+           "gflops": round(2.0 * st["nr_nzeros"] / (ms * 1e-3) / 1e9, 3),
+           "alg_GBps": round(st["algorithmic_bytes"] / (ms * 1e-3) / 1e9, 2),
+           "device_bytes": st["device_bytes"], "max_rel_diff_vs_value_kernel": diff}
+    plan.destroy()
+    del y
+    torch.cuda.empty_cache()
+    return res
+
+
 def strong_companion(lib, args, world, rank, dev, stream):
     """Config 4 beside a weak-scaling run: the SAME 10M/160M matrix cut into `world` nnz-balanced
     row slices (one per rank), timed like the headline (warm-up, barrier-bracketed K steps, max
@@ -247,7 +294,8 @@ def main():
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
     keep_csr = rank == 0 and world == 1 and not args.no_cpu
-    if not keep_csr:
+    want_xtiles = world == 1 and args.workload == "powerlaw" and not args.no_xtiles
+    if not keep_csr and not want_xtiles:
         del rp, col, val
         torch.cuda.empty_cache()
 
@@ -269,6 +317,13 @@ def main():
     ms_local = (t1 - t0) * 1e3 / args.steps
     ms = spmv_dist.max_over_ranks(ms_local, dev)
     kernel_ms_max = spmv_dist.max_over_ranks(kernel_ms, dev)
+
+    xtiles = None
+    if want_xtiles:
+        xtiles = lds_xtiles(lib, args, rp, col, val, x, y, ncols, local, stream)
+        if not keep_csr:
+            del rp, col, val
+            torch.cuda.empty_cache()
 
     # iterative / persistent mode: the same K SpMVs replayed from one hipGraph
     # (reported beside the headline, which stays one host launch per step)
@@ -443,6 +498,7 @@ def main():
             "exchange": exchange,
             "graph": graph,
             "strong_companion": strong,
+            "lds_xtiles": xtiles,
             "host_copy": host,
             "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
             "setup_s": round(setup_s, 2),
