@@ -110,6 +110,8 @@ static int requested_kernel()
         return kKernelFpga;
     if (!std::strcmp(e, "blocked"))
         return kKernelBlocked;
+    if (!std::strcmp(e, "slices"))
+        return kKernelSlices;
     return -1;
 }
 
@@ -370,7 +372,15 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
         else if (rc)
             return 1;
     }
-    if (kernel == kKernelBlocked) {
+    if (kernel == kKernelSlices) {
+        const int rc = build_slices(P, h_row_ptr, d_col, d_val, s);
+        if (rc == 2 && automatic)
+            P.kernel = kernel = kKernelTiles;
+        else if (rc)
+            return 1;
+    }
+    if (kernel == kKernelSlices) {
+    } else if (kernel == kKernelBlocked) {
         if (fpga_params(P) || build_blocked(P, h_row_ptr, d_col, d_val, s))
             return 1;
     } else if (kernel == kKernelGold || kernel == kKernelFpga) {
@@ -389,6 +399,8 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
         (void)launch_sweep(P, nullptr, nullptr, s, true);
     } else if (P.kernel == kKernelBlocked) {
         (void)launch_blocked(P, nullptr, nullptr, s, true);
+    } else if (P.kernel == kKernelSlices) {
+        (void)launch_slices(P, nullptr, nullptr, s, true);
     } else if (P.kernel == kKernelGold || P.kernel == kKernelFpga) {
         (void)launch_gold(P, nullptr, nullptr, s, true);
     } else {
@@ -506,8 +518,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         if (v == 256 || v == 512 || v == 1024)
             p->sweep_threads = v;
     }
-    if (kernel == kKernelTune) {
-        // build both layouts, time one SpMV of each on this matrix, keep the faster
+    auto fresh = [&]() {
         std::unique_ptr<spmv_plan> q(new spmv_plan());
         q->device = p->device;
         q->nr_rows = p->nr_rows;
@@ -516,22 +527,55 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         q->nzr = p->nzr;
         q->has_empty = p->has_empty;
         q->sweep_threads = p->sweep_threads;
+        q->locality = p->locality;
+        return q;
+    };
+    if (kernel == kKernelTune) {
+        // build the tile, sweep and slice layouts, time one SpMV of each on this matrix, keep
+        // the fastest
+        std::unique_ptr<spmv_plan> q = fresh(), r = fresh();
         if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s) ||
-            build_layout(*q, kKernelSweep, true, h_row_ptr, d_col, d_val, s))
+            build_layout(*q, kKernelSweep, true, h_row_ptr, d_col, d_val, s) ||
+            build_layout(*r, kKernelSlices, true, h_row_ptr, d_col, d_val, s))
             return 1;
         Tmp tx, ty;
         SPMV_TRY(hipMalloc(&tx.p, std::max<size_t>(nr_cols, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMalloc(&ty.p, std::max<size_t>(nr_rows, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMemsetAsync(tx.p, 0, std::max<size_t>(nr_cols, 1) * sizeof(ValueType), s));
-        double mt = 1e30, ms = 1e30;
+        double mt = 1e30, ms = 1e30, ml = 1e30;
         if (time_layout(*p, (const ValueType *)tx.p, (ValueType *)ty.p, s, &mt) ||
-            time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ms))
+            time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ms) ||
+            time_layout(*r, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ml))
             return 1;
-        if (ms < mt)
+        if (ms < mt && ms <= ml)
             p.swap(q);
+        else if (ml < mt && ml < ms)
+            p.swap(r);
         p->tuned_ms[0] = mt;
         p->tuned_ms[1] = ms;
-        trace("tune: build both + time", s);
+        p->tuned_ms[2] = ml;
+        trace("tune: build all + time", s);
+    } else if (requested_kernel() < 0 && kernel == kKernelTiles && nnz >= 65536) {
+        // automatic, local columns: the slice layout when rows of a 64-row slice have about the
+        // same length (<= 15 % padding) and every slot fits 16-bit (or clustered 16-bit) offsets
+        // -- finite-element / stencil-like matrices, where it is 7-14 % faster than the tiles
+        // (fp32: 24-34 %, profiles/r01_ab_variants.jsonl); in fp64, 8-bit spans (narrow bands)
+        // keep the tiles, which gather a band's x from fewer lines per instruction (the fp32
+        // band is 13 % faster in slices)
+        std::unique_ptr<spmv_plan> r = fresh();
+        const int rc = build_layout(*r, kKernelSlices, true, h_row_ptr, d_col, d_val, s);
+        if (rc == 0 && r->kernel == kKernelSlices &&
+            (r->slice_off_bytes == 2 || (r->slice_off_bytes == 1 && sizeof(ValueType) == 4)) &&
+            double(r->slice_slots) * kWave <= 1.15 * double(nnz)) {
+            p.swap(r);
+            trace("build slice layout", s);
+        } else {
+            r.reset();
+            (void)hipGetLastError();
+            if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s))
+                return 1;
+            trace("build tile layout", s);
+        }
     } else {
         if (build_layout(*p, kernel, requested_kernel() < 0, h_row_ptr, d_col, d_val, s))
             return 1;
@@ -554,7 +598,8 @@ spmv_plan::~spmv_plan()
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
                       (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
-                      (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart})
+                      (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
+                      (void *)d_sbase, (void *)d_slice_len})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -569,6 +614,10 @@ uint64_t spmv_plan::device_bytes() const
 {
     if (kernel == kKernelGold || kernel == kKernelFpga)
         return (uint64_t(nr_rows) + 1) * 4 + nnz * (4 + sizeof(ValueType));
+    if (kernel == kKernelSlices)  // padded entries, slot bases, slice offsets, row lengths
+        return slice_slots * kWave * (sizeof(ValueType) + slice_off_bytes) + slice_slots * (slice_clustered ? 16 : 4) +
+               (nslices + 1) * 4 +
+               uint64_t(nr_rows) * 4;
     if (kernel == kKernelBlocked)  // entries, kptr, kpos, rl, partials, rp2, chunks, units
         return nnz * (2 + sizeof(ValueType)) + (nkpairs + 1) * 4 + nkpairs * (4 + 2 + sizeof(ValueType)) +
                (uint64_t(nr_rows) + 1) * 4 + (nchunks + 1) * 4 + nunits * 8 + 4;
@@ -662,6 +711,7 @@ static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStrea
     if (p->kernel != kKernelTiles) {
         SPMV_TRY(p->kernel == kKernelSweep     ? launch_sweep(*p, d_x, d_y, s)
                  : p->kernel == kKernelBlocked ? launch_blocked(*p, d_x, d_y, s)
+                 : p->kernel == kKernelSlices  ? launch_slices(*p, d_x, d_y, s)
                                                : launch_gold(*p, d_x, d_y, s));
         if (timing)
             SPMV_TRY(hipEventRecord(e1, s));
@@ -750,8 +800,12 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->nr_nonempty_rows = p->nzr;
     // work units of the main kernel: tiles, sweep units (panel pieces), or long rows (gold)
     const bool csr = p->kernel == kKernelGold || p->kernel == kKernelFpga;
-    st->nr_tiles = (p->kernel == kKernelSweep || p->kernel == kKernelBlocked) ? p->nunits : csr ? p->nlong : p->ntiles;
-    st->tile_nnz = p->kernel == kKernelSweep     ? (p->nunits ? p->ent_pad / p->nunits : 0)
+    st->nr_tiles = (p->kernel == kKernelSweep || p->kernel == kKernelBlocked) ? p->nunits
+                   : p->kernel == kKernelSlices                               ? p->nslices
+                   : csr                                                      ? p->nlong
+                                                                              : p->ntiles;
+    st->tile_nnz = p->kernel == kKernelSlices   ? p->slice_slots * kWave  // stored entries with padding
+                   : p->kernel == kKernelSweep  ? (p->nunits ? p->ent_pad / p->nunits : 0)
                    : p->kernel == kKernelBlocked ? (p->nunits ? p->nnz / p->nunits : 0)
                    : csr                         ? (uint64_t)kGoldLong
                                                  : kTileNnz;
@@ -760,7 +814,8 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->device = p->device;
     st->kernel = p->kernel;
     st->blocks = p->kernel == kKernelBlocked ? (uint32_t)((uint64_t(p->nr_cols) + p->fpga_width - 1) / p->fpga_width) : 1;
-    st->format = (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) |
+    st->format = (p->kernel == kKernelSlices && p->slice_off_bytes < 4 ? 1 : 0) | (p->slice_clustered ? 16 : 0) |
+                 (p->kernel == kKernelSlices && p->slice_off_bytes == 1 ? 8 : 0) | (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) |
                  (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0);
     return 0;
 }

@@ -48,6 +48,7 @@ constexpr int kKernelSweep = 2;  // panel sweep: y in LDS, columns swept in orde
 constexpr int kKernelFpga = 3;   // the reference FPGA path's order for (VF, block width), bitwise
 constexpr int kKernelBlocked = 4;  // the same order by the reference's dataflow: x blocks in LDS,
                                    // per-block partials, block-ordered merge (blocked.hip)
+constexpr int kKernelSlices = 5;   // wave per 64 rows, entries slot-major (slices.hip)
 constexpr int kGoldLong = 128;   // gold plan stats: rows longer than this count as long
 
 }  // namespace spmvhw
@@ -97,6 +98,14 @@ struct spmv_plan {
     uint64_t nkpairs = 0, nchunks = 0;
     bool blocked_xlds = false;        // x block staged in LDS (W * sizeof(V) <= 128 KiB)
 
+    // slice representation (kernel 5, slices.hip): slot-major entries in d_val / d_colnar
+    uint32_t *d_slot_off = nullptr;   // slots of each 64-row slice [nslices + 1]
+    uint32_t *d_sbase = nullptr;      // base column of each slot
+    uint32_t *d_slice_len = nullptr;  // row lengths
+    uint64_t nslices = 0, slice_slots = 0;
+    int slice_off_bytes = 4;          // 1, 2 (offsets from the slot base) or 4 (absolute columns)
+    bool slice_clustered = false;     // 2-byte offsets as (cluster << 14) | offset, 4 bases per slot
+
     // panel-sweep representation (kernel 2, sweep.hip)
     uint64_t npanels = 0, ent_pad = 0;
     uint64_t nunits = 0;               // workgroups of a launch = npanels * sweep_split
@@ -115,7 +124,7 @@ struct spmv_plan {
     bool sweep_packed = false;
     bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)
     double locality = -1.0;    // probe result used by the automatic kernel choice
-    double tuned_ms[2] = {-1.0, -1.0};  // SPMV_HW_KERNEL=tune: measured tiles / sweep ms
+    double tuned_ms[3] = {-1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: measured tiles / sweep / slices ms
 
     // timing (HIP events around the main kernel, on the launch stream)
     bool timing = false;
@@ -179,6 +188,11 @@ hipError_t launch_gold(const spmv_plan &p, const ValueType *d_x, ValueType *d_y,
 hipError_t launch_blocked(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
 int build_blocked(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                   hipStream_t s);
+
+// slices.hip
+hipError_t launch_slices(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
+int build_slices(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
+                 hipStream_t s);
 
 // sweep.hip
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
