@@ -374,6 +374,10 @@ def main():
         kname = "k_spmv_gold"
     elif st["kernel"] == 3:
         kname = "k_spmv_fpga"
+    elif st["kernel"] == 4:
+        kname = "k_blocked_partials"
+    elif st["kernel"] == 5:
+        kname = "k_spmv_slices"
     else:
         kname = "k_spmv_tiles"
     traffic = None
