@@ -563,6 +563,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         // keep the tiles, which gather a band's x from fewer lines per instruction (the fp32
         // band is 13 % faster in slices)
         std::unique_ptr<spmv_plan> r = fresh();
+        r->slice_pad_limit = 1.15;
         const int rc = build_layout(*r, kKernelSlices, true, h_row_ptr, d_col, d_val, s);
         if (rc == 0 && r->kernel == kKernelSlices &&
             (r->slice_off_bytes == 2 || (r->slice_off_bytes == 1 && sizeof(ValueType) == 4)) &&

@@ -346,6 +346,10 @@ int build_slices(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         }
     }
     so[S] = (uint32_t)slots;
+    if (p.slice_pad_limit > 0.0 && double(slots) * kWave > p.slice_pad_limit * double(p.nnz)) {
+        set_error("slices: padding above the automatic choice's limit");
+        return 2;  // decided from row_ptr alone, before any allocation
+    }
     p.nslices = S;
     p.slice_slots = slots;
     const uint64_t E = slots * kWave;
