@@ -570,6 +570,10 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             double(r->slice_slots) * kWave <= 1.15 * double(nnz)) {
             p.swap(r);
             trace("build slice layout", s);
+        } else if (rc == 0 && r->kernel == kKernelTiles) {  // padding too high: built as tiles
+            r->slice_pad_limit = 0.0;
+            p.swap(r);
+            trace("build tile layout", s);
         } else {
             r.reset();
             (void)hipGetLastError();
