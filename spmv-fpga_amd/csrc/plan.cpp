@@ -365,21 +365,18 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
                         const IndexType *d_col, const ValueType *d_val, hipStream_t s)
 {
     P.kernel = kernel;
-    if (kernel == kKernelSweep) {
-        const int rc = build_sweep(P, h_row_ptr, d_col, d_val, s);
-        if (rc == 2 && automatic)
-            P.kernel = kernel = kKernelTiles;  // the tile layout has no 32-bit entry-offset limit
-        else if (rc)
-            return 1;
-    }
-    if (kernel == kKernelSlices) {
-        const int rc = build_slices(P, h_row_ptr, d_col, d_val, s);
+    if (kernel == kKernelSweep || kernel == kKernelSlices) {
+        // rc 2: the layout cannot hold this matrix (32-bit entry offsets, or the automatic
+        // choice's padding limit); automatic plans fall back to the tiles, which have neither
+        const int rc = kernel == kKernelSweep ? build_sweep(P, h_row_ptr, d_col, d_val, s)
+                                              : build_slices(P, h_row_ptr, d_col, d_val, s);
         if (rc == 2 && automatic)
             P.kernel = kernel = kKernelTiles;
         else if (rc)
             return 1;
     }
-    if (kernel == kKernelSlices) {
+    if (kernel == kKernelSweep || kernel == kKernelSlices) {
+        // built above
     } else if (kernel == kKernelBlocked) {
         if (fpga_params(P) || build_blocked(P, h_row_ptr, d_col, d_val, s))
             return 1;
@@ -388,7 +385,7 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
             return 1;
         if (kernel == kKernelFpga && order_rows_by_block(P, h_row_ptr, s))
             return 1;
-    } else if (kernel != kKernelSweep) {
+    } else {
         if (build_tiles(P, h_row_ptr, d_col, d_val, s))
             return 1;
     }
