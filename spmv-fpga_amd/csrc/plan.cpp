@@ -626,7 +626,7 @@ uint64_t spmv_plan::device_bytes() const
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
-               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * 8 : 0) + nunits * 4 + (npanels + 1) * 4;
+               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * sweep_acc_bytes : 0) + nunits * 4 + (npanels + 1) * 4;
     return nnz_pad * (tile_col_bytes + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
            (tile_col_bytes < 4 ? ntiles * (tile_clustered ? 16 : 4) : 0) +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;

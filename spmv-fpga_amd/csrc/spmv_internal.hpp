@@ -113,7 +113,8 @@ struct spmv_plan {
     uint32_t sweep_split = 1;          // > 1: some panel is cut into pieces (partials + combine)
     uint32_t *d_unit_panel = nullptr;  // panel of each work unit
     uint32_t *d_panel_unit = nullptr;  // first unit of each panel [npanels + 1]
-    double *d_part = nullptr;          // split > 1: nunits x (panel_rmax + 1) fp64 partial sums
+    void *d_part = nullptr;            // split > 1: nunits x (panel_rmax + 1) partial sums (accumulator type)
+    int sweep_acc_bytes = 8;           // LDS accumulator: 8 (fp64) or 4 (fp32 via CAS, env SPMV_SWEEP_ACC=32)
     uint32_t panel_rmax = 0;
     int sweep_threads = spmvhw::kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)
     uint32_t *d_s_col = nullptr;

@@ -34,10 +34,54 @@
 
 namespace spmvhw {
 
-// The LDS accumulator is fp64 for both precisions: gfx950 executes ds_add_f32 about 8x slower
-// than ds_add_f64 (SQ_LDS_IDX_ACTIVE of the fp32 sweep ~95% of its cycles, profiles/), and
-// fp32 products are exact in fp64, so y of an fp32 matrix is the fp64 sum rounded once.
-typedef double SweepAcc;
+// LDS accumulator A: fp64 (ds_add_f64) for both precisions by default; fp32 products are exact
+// in fp64, so y of an fp32 matrix is the fp64 sum rounded once. An fp32 accumulator would let a
+// panel hold twice the rows (40,895 instead of 20,447: denser panels), but gfx950 executes the
+// native ds_add_f32 ~8x slower than ds_add_f64 at random rows (203 vs 1660 G adds/s,
+// tools/lds_atomics.hip). A compare-and-swap loop on the float's bits matches ds_add_f64 in
+// that microbenchmark, and env SPMV_SWEEP_ACC=32 selects it here; on the 10M/160M fp32 matrix
+// it measured 1.94 ms against 0.60 ms for the fp64 accumulator (the CAS round trips serialise
+// each wave: 1.04 ms without any gathers; profiles/r01_ab_variants.jsonl, session r01c_acc).
+__device__ __forceinline__ void lds_add(double *p, double v) { atomicAdd(p, v); }
+__device__ __forceinline__ void lds_add(float *p, float v)
+{
+    uint32_t *u = reinterpret_cast<uint32_t *>(p);
+    uint32_t old = *u, assumed;
+    do {
+        assumed = old;
+        old = atomicCAS(u, assumed, __float_as_uint(__uint_as_float(assumed) + v));
+    } while (old != assumed);
+}
+
+// N adds of one lane at once: fp64 = N fire-and-forget ds_add_f64; fp32 = N reads, then N
+// compare-and-swaps in flight together, then a retry loop for the (rare) ones another lane or
+// wave got in between -- two LDS round trips per batch instead of two per add
+template <int N>
+__device__ __forceinline__ void lds_add_n(double *y, const uint32_t (&idx)[N], const double (&v)[N])
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        atomicAdd(&y[idx[i]], v[i]);
+}
+template <int N>
+__device__ __forceinline__ void lds_add_n(float *y, const uint32_t (&idx)[N], const float (&v)[N])
+{
+    uint32_t *u = reinterpret_cast<uint32_t *>(y);
+    uint32_t old[N], got[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        old[i] = __hip_atomic_load(&u[idx[i]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        got[i] = atomicCAS(&u[idx[i]], old[i], __float_as_uint(__uint_as_float(old[i]) + v[i]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        while (got[i] != old[i]) {
+            old[i] = got[i];
+            got[i] = atomicCAS(&u[idx[i]], old[i], __float_as_uint(__uint_as_float(old[i]) + v[i]));
+        }
+    }
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
@@ -98,15 +142,15 @@ __device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o
 // A unit's y: stored when the panel is one unit; a panel cut into pieces has each piece store
 // its fp64 partial sums (its column range) into part[unit * stride + i], and k_sweep_combine
 // adds the pieces of every row in piece order (deterministic, one rounding).
-template <typename V, int T>
-__device__ __forceinline__ void write_panel(const SweepAcc *__restrict__ ylds, uint32_t R, V *__restrict__ y,
-                                            uint32_t pieces, SweepAcc *__restrict__ part, uint32_t stride)
+template <typename V, int T, typename A>
+__device__ __forceinline__ void write_panel(const A *__restrict__ ylds, uint32_t R, V *__restrict__ y,
+                                            uint32_t pieces, A *__restrict__ part, uint32_t stride)
 {
     if (pieces == 1) {
         for (uint32_t i = threadIdx.x; i < R; i += T)
             y[i] = V(ylds[i]);
     } else {
-        SweepAcc *dst = part + (uint64_t)blockIdx.x * stride;
+        A *dst = part + (uint64_t)blockIdx.x * stride;
         for (uint32_t i = threadIdx.x; i < R; i += T)
             dst[i] = ylds[i];
     }
@@ -114,10 +158,10 @@ __device__ __forceinline__ void write_panel(const SweepAcc *__restrict__ ylds, u
 
 // y[r0 + i] = sum over the panel's pieces u (in order) of part[u * stride + i]; panels of one
 // piece were written by the sweep itself
-template <typename V>
+template <typename V, typename A>
 __global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restrict__ panel_row,
                                                        const uint32_t *__restrict__ panel_unit,
-                                                       const SweepAcc *__restrict__ part, uint32_t stride,
+                                                       const A *__restrict__ part, uint32_t stride,
                                                        V *__restrict__ y)
 {
     const uint32_t p = blockIdx.y;
@@ -126,8 +170,8 @@ __global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restric
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (u1 - u0 < 2 || i >= R)
         return;
-    const SweepAcc *src = part + (uint64_t)u0 * stride + i;
-    SweepAcc acc = src[0];
+    const A *src = part + (uint64_t)u0 * stride + i;
+    A acc = src[0];
     for (uint32_t t = 1; t < u1 - u0; ++t)
         acc += src[(uint64_t)t * stride];
     y[r0 + i] = V(acc);
@@ -136,23 +180,23 @@ __global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restric
 // E entries per thread per workgroup iteration, Q such groups per iteration; SYNC: barrier after
 // every iteration so the 16 waves stay on one column window; NT: non-temporal entry loads.
 // Entry ranges of a panel are multiples of 4, so whole E-groups are always valid.
-template <typename V, int T, int E, int Q, bool SYNC, bool NT>
+template <typename V, int T, int E, int Q, bool SYNC, bool NT, typename A = double>
 __global__ __launch_bounds__(T) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
-    SweepAcc *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
+    A *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef typename EntryVec<E>::C CV;
     typedef typename EntryVec<E>::R RV;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
+    A *ylds = reinterpret_cast<A *>(smem);
     const uint32_t p = unit_panel[blockIdx.x];  // unit = a piece of a panel's column-sorted entries
     const uint32_t pieces = panel_unit[p + 1] - panel_unit[p];
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     for (uint32_t i = threadIdx.x; i <= R; i += T)
-        ylds[i] = SweepAcc(0);
+        ylds[i] = A(0);
     __syncthreads();
     constexpr uint64_t kGroup = (uint64_t)E * T;  // entries per workgroup group
     // branch-free body (see k_spmv_sweep_packed): out-of-range groups re-read the panel's last
@@ -182,12 +226,12 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
         for (int q = 0; q < Q; ++q)
 #pragma unroll
             for (int j = 0; j < E; ++j)
-                atomicAdd(&ylds[ok[q] ? (uint32_t)r[q][j] : R], SweepAcc(v[q][j]) * SweepAcc(xv[q][j]));
+                lds_add(&ylds[ok[q] ? (uint32_t)r[q][j] : R], A(v[q][j]) * A(xv[q][j]));
         if constexpr (SYNC)
             __syncthreads();
     }
     __syncthreads();
-    write_panel<V, T>(ylds, R, y + r0, pieces, part, stride);
+    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
 }
 
 // Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
@@ -196,28 +240,28 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
 // LAG = 0: one workgroup barrier per iteration. LAG = k > 0: no barrier; each wave publishes
 // its iteration count in LDS and only waits (s_sleep) while it is more than k iterations
 // ahead of the slowest wave, so the vector-memory pipe never drains at a common barrier.
-template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0>
+template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
-    SweepAcc *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
+    A *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    SweepAcc *ylds = reinterpret_cast<SweepAcc *>(smem);
+    A *ylds = reinterpret_cast<A *>(smem);
     const uint32_t p = unit_panel[blockIdx.x];  // unit = a piece of a panel's column-sorted entries
     const uint32_t pieces = panel_unit[p + 1] - panel_unit[p];
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     __shared__ uint32_t progress[T / 64];
     for (uint32_t i = threadIdx.x; i <= R; i += T)
-        ylds[i] = SweepAcc(0);
+        ylds[i] = A(0);
     if (threadIdx.x < T / 64)
         progress[threadIdx.x] = 0;
     __syncthreads();
     uint32_t iter = 0;
-    SweepAcc sink = 0;  // ablations 8/9 only
+    A sink = 0;  // ablations 8/9 only
     constexpr uint64_t kGroup = 2ull * T;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane2 = 2u * (threadIdx.x & 63);
@@ -261,14 +305,21 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
                 xv[q][1] = x[(cb[q] + (w[q].y & 0xFFFFu)) & m];
             }
         }
+        if constexpr (ABL == 8 || ABL == 9) {  // ablation: no LDS adds (register sum)
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if constexpr (ABL == 8 || ABL == 9) {  // ablation: no LDS adds (register sum)
-                sink += SweepAcc(v[q][0]) * SweepAcc(xv[q][0]) + SweepAcc(v[q][1]) * SweepAcc(xv[q][1]);
-            } else {
-                atomicAdd(&ylds[ok[q] ? (w[q].x >> 16) : R], SweepAcc(v[q][0]) * SweepAcc(xv[q][0]));
-                atomicAdd(&ylds[ok[q] ? (w[q].y >> 16) : R], SweepAcc(v[q][1]) * SweepAcc(xv[q][1]));
+            for (int q = 0; q < Q; ++q)
+                sink += A(v[q][0]) * A(xv[q][0]) + A(v[q][1]) * A(xv[q][1]);
+        } else {
+            uint32_t ri[2 * Q];
+            A pv[2 * Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                ri[2 * q] = ok[q] ? (w[q].x >> 16) : R;
+                ri[2 * q + 1] = ok[q] ? (w[q].y >> 16) : R;
+                pv[2 * q] = A(v[q][0]) * A(xv[q][0]);
+                pv[2 * q + 1] = A(v[q][1]) * A(xv[q][1]);
             }
+            lds_add_n<2 * Q>(ylds, ri, pv);
         }
         if constexpr (LAG == 0) {
             __syncthreads();
@@ -294,9 +345,9 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         }
     }
     if constexpr (ABL == 8 || ABL == 9)
-        atomicAdd(&ylds[R], sink);
+        lds_add(&ylds[R], sink);
     __syncthreads();
-    write_panel<V, T>(ylds, R, y + r0, pieces, part, stride);
+    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
 }
 
 // chunk c of 128 entries: base = min column; fails the plan's packing when the span >= 65536
@@ -441,21 +492,23 @@ __global__ void k_locality(const IndexType *__restrict__ rp, const IndexType *__
     atomicAdd(&counts[1], near);
 }
 
-template <int T>
+template <int T, typename A>
 static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
 {
-    const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(SweepAcc);
+    const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(A);
     const dim3 grid((unsigned)p.nunits), block(T);
+    A *part = reinterpret_cast<A *>(p.d_part);
     // Unpacked (14-B entries, used when a chunk spans >= 65536 columns): E entries per thread,
     // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
-    launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT>, grid, block, lds, s, p.d_s_col,   \
-                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
+    launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT, A>, grid, block, lds, s, p.d_s_col,   \
+                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, d_x, d_y)
     if (p.sweep_packed) {
-#define PKN(NT, Q, LAG, ...)                                                                        \
-    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG __VA_OPT__(,) __VA_ARGS__>, grid, block, lds, s, p.d_s_col, \
-                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, p.d_part, p.panel_rmax + 1, d_x, d_y)
-#define PK(Q, LAG, ...) PKN(true, Q, LAG __VA_OPT__(,) __VA_ARGS__)
+#define PKN(NT, Q, LAG, ABL)                                                                        \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
+                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, d_x, d_y)
+#define PK(Q, LAG) PKN(true, Q, LAG, 0)
+#define PKA(ABL) PKN(true, 2, 2, ABL)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
         case 15: PK(2, 0); break;
@@ -469,18 +522,20 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 32: PK(1, 2); break;
         case 33: PK(1, 4); break;
         case 34: PK(2, 3); break;
-        case 60: if (p.nr_cols >= 32768) { PK(2, 2, 1); } else { PK(2, 2); } break;  // ablation: x gathers all L2 hits (wrong y; measurement only)
-        case 61: PK(2, 2, 2); break;  // ablation: no x gathers (wrong y; measurement only)
-        case 62: PK(2, 2, 3); break;  // ablation: entries from L2 (first 4K of the unit), real gathers
-        case 63: if (p.nr_cols >= 32768) { PK(2, 2, 4); } else { PK(2, 2); } break;  // entries + x from L2
+        // measurement-only ablations (54, 55, 60-63 give wrong y by design), DESIGN.md §4
+        case 60: if (p.nr_cols >= 32768) { PKA(1); } else { PK(2, 2); } break;  // x gathers all L2 hits
+        case 61: PKA(2); break;  // no x gathers
+        case 62: PKA(3); break;  // entries from L2 (first 4K of the unit), real gathers
+        case 63: if (p.nr_cols >= 32768) { PKA(4); } else { PK(2, 2); } break;  // entries + x from L2
         case 59: PK(2, 1000); break;  // no wave sync (lag never reached)
-        case 56: PKN(false, 2, 2); break;  // plain (temporal) entry loads
-        case 54: PK(2, 2, 8); break;  // ablation: no LDS adds
-        case 55: if (p.nr_cols >= 32768) { PK(2, 2, 9); } else { PK(2, 2); } break;  // no LDS adds, all L2
-        case 57: PK(2, 2, 6); break;  // x gathers with the nt bit
-        case 58: PK(2, 2, 7); break;  // x gathers that bypass L1 (sc1)
+        case 56: PKN(false, 2, 2, 0); break;  // plain (temporal) entry loads
+        case 54: PKA(8); break;  // no LDS adds
+        case 55: if (p.nr_cols >= 32768) { PKA(9); } else { PK(2, 2); } break;  // no LDS adds, all L2
+        case 57: PKA(6); break;  // x gathers with the nt bit
+        case 58: PKA(7); break;  // x gathers that bypass L1 (sc1)
         default: PK(2, 2); break;
         }
+#undef PKA
 #undef PK
 #undef PKN
         return;
@@ -497,20 +552,32 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #undef SWEEP
 }
 
+template <typename A>
+static void launch_sweep_a(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
+{
+    switch (p.sweep_threads) {
+    case 256: launch_sweep_t<256, A>(p, d_x, d_y, s, warm); break;
+    case 512: launch_sweep_t<512, A>(p, d_x, d_y, s, warm); break;
+    default: launch_sweep_t<1024, A>(p, d_x, d_y, s, warm); break;
+    }
+    if (p.sweep_split > 1) {
+        const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
+        launch_or_warm(warm, k_sweep_combine<ValueType, A>, grid, dim3(256), 0, s, p.d_panel_row, p.d_panel_unit,
+                       reinterpret_cast<const A *>(p.d_part), p.panel_rmax + 1, d_y);
+    }
+}
+
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
 {
     if (p.npanels == 0)
         return hipSuccess;
-    switch (p.sweep_threads) {
-    case 256: launch_sweep_t<256>(p, d_x, d_y, s, warm); break;
-    case 512: launch_sweep_t<512>(p, d_x, d_y, s, warm); break;
-    default: launch_sweep_t<1024>(p, d_x, d_y, s, warm); break;
+    if constexpr (sizeof(ValueType) == 4) {
+        if (p.sweep_acc_bytes == 4) {
+            launch_sweep_a<float>(p, d_x, d_y, s, warm);
+            return hipGetLastError();
+        }
     }
-    if (p.sweep_split > 1) {
-        const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
-        launch_or_warm(warm, k_sweep_combine<ValueType>, grid, dim3(256), 0, s, p.d_panel_row, p.d_panel_unit,
-                           p.d_part, p.panel_rmax + 1, d_y);
-    }
+    launch_sweep_a<double>(p, d_x, d_y, s, warm);
     return hipGetLastError();
 }
 
@@ -530,7 +597,11 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     const uint64_t nnz = p.nnz;
     // a workgroup of T threads gets T/1024 of one CU's LDS for its panel's y
     const uint64_t lds_bytes = kSweepLdsBytes * p.sweep_threads / 1024 - 256;  // 256 B: static LDS
-    const uint32_t rmax = (uint32_t)std::min<uint64_t>(lds_bytes / sizeof(SweepAcc) - 1, 65534);
+    // accumulator: fp64, or fp32 (compare-and-swap adds) for fp32 matrices with env SPMV_SWEEP_ACC=32
+    const char *aenv = std::getenv("SPMV_SWEEP_ACC");
+    p.sweep_acc_bytes = sizeof(ValueType) == 4 && aenv && std::atoi(aenv) == 32 ? 4 : 8;
+    const uint64_t acc = p.sweep_acc_bytes;
+    const uint32_t rmax = (uint32_t)std::min<uint64_t>(lds_bytes / acc - 1, 65534);
     int cus = 256;
     {
         hipDeviceProp_t prop;
@@ -553,7 +624,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             // the 10M/160M matrix 18 % (0.33x), a 300K-row matrix 25 % slower (1.4x)
             const uint64_t S = P ? (uint64_t)cus / P : 0;
             split_mode = allow_split && S >= 2 && P * S * 10 >= (uint64_t)cus * 9 &&
-                         (force_split || 2 * S * n * sizeof(SweepAcc) * 5 <= 3 * nnz * (4 + sizeof(ValueType)));
+                         (force_split || 2 * S * n * acc * 5 <= 3 * nnz * (4 + sizeof(ValueType)));
         }
         if (!split_mode && P > 1 && P % cus)
             P = (P + cus - 1) / cus * cus;  // whole rounds of workgroups
@@ -629,7 +700,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     p.sweep_split = multi ? std::max<uint32_t>(split, 2) : 1;  // > 1: combine kernel needed
     p.nunits = U;
     if (multi)
-        SPMV_TRY(hipMalloc((void **)&p.d_part, (uint64_t)U * (uint64_t(rmax_used) + 1) * sizeof(SweepAcc)));
+        SPMV_TRY(hipMalloc((void **)&p.d_part, (uint64_t)U * (uint64_t(rmax_used) + 1) * acc));
     SPMV_TRY(hipMalloc((void **)&p.d_unit_panel, upanel.size() * 4));
     SPMV_TRY(hipMalloc((void **)&p.d_panel_unit, punit.size() * 4));
     SPMV_TRY(hipMemcpyAsync(p.d_unit_panel, upanel.data(), upanel.size() * 4, hipMemcpyHostToDevice, s));
