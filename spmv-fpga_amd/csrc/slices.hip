@@ -74,8 +74,9 @@ struct SliceOff<4> {  // absolute 32-bit columns (sbase = 0), when a slot spans 
 };
 
 // PU pairs of slots per iteration; every load of the iteration is issued before the first
-// gather (pairs past the slice's end re-read its first pair and add nothing)
-template <typename V, int OB, int PU>
+// gather (pairs past the slice's end re-read its first pair and add nothing; TAIL: they are
+// skipped by a wave-uniform branch instead)
+template <typename V, int OB, int PU, bool TAIL = false>
 __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restrict__ val, const void *__restrict__ offv,
                                                              const uint32_t *__restrict__ sbase,
                                                              const uint32_t *__restrict__ slot_off,
@@ -102,6 +103,12 @@ __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restri
         uint32_t b0[PU], b1[PU];
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
+            if (TAIL && p + u >= npairs) {  // wave-uniform
+                v[u] = VT(0);
+                o[u] = OT(0);
+                b0[u] = b1[u] = 0u;
+                continue;
+            }
             const uint32_t pp = p + u < npairs ? p + u : 0u;  // wave-uniform
             const uint64_t e = (uint64_t)(j0 + 2 * pp) * kWave + 2 * lane;
             v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + e));
@@ -158,10 +165,24 @@ hipError_t launch_slices(const spmv_plan &p, const ValueType *d_x, ValueType *d_
         return hipSuccess;
     const uint32_t nsl = (uint32_t)p.nslices;
     const dim3 grid((nsl + kSliceThreads / kWave - 1) / (kSliceThreads / kWave));
+#define SLV(OB, PU, TAIL)                                                                                        \
+    launch_or_warm(warm, k_spmv_slices<ValueType, OB, PU, TAIL>, grid, dim3(kSliceThreads), 0, s,                 \
+                   (const ValueType *)p.d_val, (const void *)p.d_colnar, (const uint32_t *)p.d_sbase,             \
+                   (const uint32_t *)p.d_slot_off, (const uint32_t *)p.d_slice_len, d_x, d_y, p.nr_rows, nsl)
+    // variant (spmv_plan_set_variant): 0 = 4 pairs per iteration, pairs past the slice's end
+    // skipped (default: 27-point 0.450 vs 0.508 ms, 7-point 0.126 vs 0.131 when they re-read the
+    // first pair); 1 = 2 pairs, 2 = 7 pairs, 3 = 4 pairs re-reading
 #define SL(OB)                                                                                                   \
-    launch_or_warm(warm, k_spmv_slices<ValueType, OB, 4>, grid, dim3(kSliceThreads), 0, s, (const ValueType *)p.d_val, \
-                   (const void *)p.d_colnar, (const uint32_t *)p.d_sbase, (const uint32_t *)p.d_slot_off,         \
-                   (const uint32_t *)p.d_slice_len, d_x, d_y, p.nr_rows, nsl)
+    do {                                                                                                         \
+        if (p.variant == 1)                                                                                      \
+            SLV(OB, 2, true);                                                                                    \
+        else if (p.variant == 2)                                                                                 \
+            SLV(OB, 7, true);                                                                                    \
+        else if (p.variant == 3)                                                                                 \
+            SLV(OB, 4, false);                                                                                   \
+        else                                                                                                     \
+            SLV(OB, 4, true);                                                                                    \
+    } while (0)
     if (p.slice_off_bytes == 1)
         SL(1);
     else if (p.slice_off_bytes == 2 && p.slice_clustered)
@@ -171,6 +192,7 @@ hipError_t launch_slices(const spmv_plan &p, const ValueType *d_x, ValueType *d_
     else
         SL(4);
 #undef SL
+#undef SLV
     return hipGetLastError();
 }
 
