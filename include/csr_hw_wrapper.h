@@ -72,22 +72,26 @@ typedef struct spmv_plan_stats {
     uint64_t nr_cols;            /* columns (length of x) */
     uint64_t nr_nzeros;          /* stored non-zeros */
     uint64_t nr_nonempty_rows;   /* rows with >= 1 non-zero */
-    uint64_t nr_tiles;           /* wave tiles of the main kernel */
-    uint64_t tile_nnz;           /* non-zeros per wave tile */
+    uint64_t nr_tiles;           /* work units of the main kernel: wave tiles (0), long rows (1, 3),
+                                    panel pieces (2), phase-1 units (4), 64-row slices (5) */
+    uint64_t tile_nnz;           /* non-zeros per unit (kernel 5: stored entries with padding) */
     uint64_t device_bytes;       /* bytes of the hw representation resident in HBM */
     uint64_t algorithmic_bytes;  /* compulsory CSR bytes per SpMV, SURVEY.md §8(d) */
     int32_t device;              /* HIP device ordinal */
     int32_t kernel;              /* 0 = flagged-tile gather, 1 = spmv_gold order (bitwise), 2 = panel
                                     sweep, 3 = the reference FPGA path's order for env
-                                    SPMV_FPGA_VF / SPMV_FPGA_BLOCK (bitwise).
-                                    Chosen automatically, or by env SPMV_HW_KERNEL = tiles |
-                                    gold | sweep | fpga | tune (build tiles and sweep, time them
-                                    on the matrix, keep the faster) */
-    int32_t blocks;              /* column blocks of the representation */
-    int32_t format;              /* bit 0: 16- or 8-bit column offsets per tile (kernel 0), bit 3:
-                                    8-bit, bit 4: 16-bit (cluster, offset) with 4 bases per tile;
-                                    bit 1: packed 12/8-byte sweep entries; bit 2: lane-ordered
-                                    chunks (kernel 2) */
+                                    SPMV_FPGA_VF / SPMV_FPGA_BLOCK (bitwise), 4 = the same order
+                                    by the reference's column-blocked dataflow (x blocks in LDS),
+                                    5 = slices (wave per 64 rows, slot-major).
+                                    Chosen automatically (0, 2 or 5), or by env SPMV_HW_KERNEL =
+                                    tiles | gold | sweep | fpga | blocked | slices | tune (build
+                                    tiles, sweep and slices, time them on the matrix, keep the
+                                    fastest) */
+    int32_t blocks;              /* column blocks of the representation (kernel 4; 1 otherwise) */
+    int32_t format;              /* bit 0: 16- or 8-bit column offsets (per tile, kernel 0; per
+                                    slot, kernel 5), bit 3: 8-bit, bit 4: 16-bit (cluster, offset)
+                                    with 4 bases per tile / slot; bit 1: packed 12/8-byte sweep
+                                    entries; bit 2: lane-ordered chunks (kernel 2) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are
@@ -113,8 +117,10 @@ int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
  * Sweep kernel, packed entries: 15/20/22 = 2/4/8 entry groups per wave per workgroup barrier;
  * 26-34 = no barrier, waves run at most 1-4 iterations ahead of the slowest wave of the
  * workgroup (26: 4 groups lag 1, 27: 4/2, 28: 2/2 = default, 29: 2/4, 30: 2/1, 31: 3/2,
- * 32: 1/2, 33: 1/4, 34: 2/3). Unpacked entries (a chunk spans >= 65536 columns): 0/1/3/7/15/22
- * and the default (4 groups of 2 per barrier). */
+ * 32: 1/2, 33: 1/4, 34: 2/3); 54-63: measurement-only ablations (54, 55 and
+ * 60-63 give a wrong y by design). Unpacked entries (a chunk spans >= 65536 columns):
+ * 0/1/3/7/15/22 and the default (4 groups of 2 per barrier). Slices (kernel 5): 0 = 4 slot
+ * pairs per iteration (default), 1 = 2, 2 = 7, 3 = 4 re-reading past the slice's end. */
 int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */
