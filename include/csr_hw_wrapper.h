@@ -120,7 +120,8 @@ int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
  * 32: 1/2, 33: 1/4, 34: 2/3); 54-63: measurement-only ablations (54, 55 and
  * 60-63 give a wrong y by design). Unpacked entries (a chunk spans >= 65536 columns):
  * 0/1/3/7/15/22 and the default (4 groups of 2 per barrier). Slices (kernel 5): 0 = 4 slot
- * pairs per iteration (default), 1 = 2, 2 = 7, 3 = 4 re-reading past the slice's end. */
+ * pairs per iteration (default), 1 = 2, 2 = 7, 3 = 4 re-reading past the slice's end.
+ * Blocked (kernel 4): 1 = measurement-only ablation, partials stored in compact order (wrong y). */
 int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */
