@@ -198,6 +198,40 @@ EDGE_CASES = {
 }
 
 
+def _structured(kind, dtype):
+    """Structured shapes with explicit columns: an arrow matrix (dense first row, dense first
+    column, diagonal), block-diagonal dense 64x64 blocks, one dense column, an upper bidiagonal
+    band with a far corner entry per row (two clusters per slot)."""
+    rng = np.random.default_rng(sum(map(ord, kind)))
+    n = 3000
+    rows = []
+    if kind == "arrow":
+        rows = [np.arange(n)] + [np.unique([0, i]) for i in range(1, n)]
+    elif kind == "block_diagonal":
+        rows = [np.arange(i // 64 * 64, min(n, i // 64 * 64 + 64)) for i in range(n)]
+    elif kind == "dense_column":
+        rows = [np.unique([7, i]) for i in range(n)]
+    elif kind == "band_plus_corner":
+        rows = [np.unique([i, min(i + 1, n - 1), (i * 7919) % n + 200_000]) for i in range(n)]
+    m = int(max(r.max() for r in rows)) + 1
+    lens = np.array([len(r) for r in rows])
+    row_ptr = np.zeros(n + 1, np.int64)
+    row_ptr[1:] = np.cumsum(lens)
+    col = np.concatenate(rows).astype(np.uint32)
+    val = rng.uniform(-1, 1, len(col)).astype(dtype)
+    x = rng.uniform(0, 1, m).astype(dtype)
+    return row_ptr.astype(np.uint32), col, val, x, m
+
+
+@pytest.mark.parametrize("kind", ["arrow", "block_diagonal", "dense_column", "band_plus_corner"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_structured_shapes(torch, kernel, kind, dtype):
+    row_ptr, col, val, x, m = _structured(kind, dtype)
+    lib = spmv_hw.load(dtype)
+    y, _ = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel=kernel)
+    check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y, dtype)
+
+
 @pytest.mark.parametrize("case", sorted(EDGE_CASES))
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_edge_cases(torch, kernel, case, dtype):
