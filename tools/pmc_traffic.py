@@ -42,7 +42,7 @@ def main():
         per_kernel = {}
         for r in rows:
             name = r["Kernel_Name"]
-            if "k_spmv_tiles" not in name and "k_spmv_sweep" not in name and "k_fixup" not in name:
+            if not any(k in name for k in ("k_spmv_tiles", "k_spmv_sweep", "k_spmv_slices", "k_fixup")):
                 continue
             short = re.sub(r"\(.*", "", name).replace("void spmvhw::", "")
             per_kernel.setdefault((short, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
