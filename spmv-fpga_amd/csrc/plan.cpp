@@ -531,6 +531,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         // build the tile, sweep and slice layouts, time one SpMV of each on this matrix, keep
         // the fastest
         std::unique_ptr<spmv_plan> q = fresh(), r = fresh();
+        r->slice_pad_limit = 2.0;  // a slice layout padded beyond 2x is built as tiles instead
         if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s) ||
             build_layout(*q, kKernelSweep, true, h_row_ptr, d_col, d_val, s) ||
             build_layout(*r, kKernelSlices, true, h_row_ptr, d_col, d_val, s))

@@ -126,6 +126,10 @@ __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restri
         V xv0[PU], xv1[PU];
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
+            if (TAIL && p + u >= npairs) {  // wave-uniform: no gather for a skipped pair
+                xv0[u] = xv1[u] = V(0);
+                continue;
+            }
             constexpr uint32_t m = OB == 3 ? 0x3FFFu : 0xFFFFFFFFu;
             xv0[u] = x[b0[u] + (o[u].x & m)];
             xv1[u] = x[b1[u] + (o[u].y & m)];
