@@ -5,6 +5,7 @@
 // BRAM, spmv.cpp:280-294). spmv_hw runs every unit's kernels, then adds each unit's y slice
 // into the caller's y_fpga (the role of accum_results, csr_hw.cpp:1531-1565, and the loop
 // csr_hw_wrapper.cpp:276-281), printing the reference's timing lines.
+#include <sys/mman.h>
 #include <sys/time.h>
 
 #include <cmath>
@@ -12,6 +13,7 @@
 #include <cstring>
 #include <iomanip>
 #include <iostream>
+#include <atomic>
 #include <mutex>
 #include <thread>
 
@@ -103,6 +105,33 @@ hipStream_t unit_stream(int unit)
     return g_streams[unit];
 }
 
+// device y and pinned staging of unit m (once per matrix)
+void alloc_y_scratch(hw_matrix_impl *m)
+{
+    const uint64_t rows = m->row_end - m->row_begin;
+    check(hipSetDevice(m->device), "hipSetDevice");
+    check(hipMalloc((void **)&m->d_y, rows * sizeof(ValueType)), "hipMalloc(y)");
+    check(hipHostMalloc((void **)&m->h_stage, rows * sizeof(ValueType), hipHostMallocDefault),
+          "hipHostMalloc(y stage)");
+}
+
+// Maps the caller's y pages writable while the DMA runs, keeping their contents: a fresh
+// calloc'd y_fpga (main.cpp:74) otherwise takes one page fault per 4 KiB inside the adds
+void prefault(ValueType *p, uint64_t count)
+{
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23  // Linux 5.14
+#endif
+    const uintptr_t pg = 4096;
+    const uintptr_t b = ((uintptr_t)p + pg - 1) & ~(pg - 1), e = (uintptr_t)(p + count) & ~(pg - 1);
+    if (e <= b || madvise((void *)b, e - b, MADV_POPULATE_WRITE) == 0)
+        return;
+    for (uintptr_t a = b; a < e; a += pg) {  // older kernels: touch each page
+        volatile ValueType *q = (volatile ValueType *)a;
+        *q = *q;
+    }
+}
+
 uint64_t ceil16(uint64_t bytes) { return (bytes + 15) / 16; }
 
 }  // namespace
@@ -147,10 +176,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         const hipStream_t us = unit_stream(u);
         const IndexType rows = h->row_end - h->row_begin;
         if (rows) {
-            check(hipSetDevice(h->device), "hipSetDevice");
-            check(hipMalloc((void **)&h->d_y, size_t(rows) * sizeof(ValueType)), "hipMalloc(y)");
-            check(hipHostMalloc((void **)&h->h_stage, size_t(rows) * sizeof(ValueType), hipHostMallocDefault),
-                  "hipHostMalloc(y stage)");
+            alloc_y_scratch(h);
             // full size: large copies take a different path whose first use costs ~20 ms
             check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
                   "warm D2H");
@@ -277,12 +303,8 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
             die("spmv_hw: y_fpga is shorter than the matrix has rows");
         if ((size_t)m->device >= x->per_device.size())
             die("spmv_hw: x vector was not uploaded to device " + std::to_string(m->device));
-        if (rows && !m->d_y) {
-            check(hipSetDevice(m->device), "hipSetDevice");
-            check(hipMalloc((void **)&m->d_y, size_t(rows) * sizeof(ValueType)), "hipMalloc(y)");
-            check(hipHostMalloc((void **)&m->h_stage, size_t(rows) * sizeof(ValueType), hipHostMallocDefault),
-                  "hipHostMalloc(y stage)");
-        }
+        if (rows && !m->d_y)
+            alloc_y_scratch(m);
     }
 
     const bool trace = std::getenv("SPMV_HW_TRACE") != nullptr;
@@ -308,7 +330,8 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
     std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
 
     // accum_results: every unit's slice comes back over its own PCIe link into pinned memory
-    // (all copies in flight together), then is added into y_fpga by a few host threads
+    // (all copies in flight together). Host threads map their part of y_fpga while the DMA
+    // runs, then add the staged slices in once every copy has landed
     const double ra_s = timestamp_us();
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
@@ -321,33 +344,49 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
               "hipMemcpyAsync(y)");
     }
     tr("spmv_hw: D2H enqueue", ra_s);
-    const unsigned hc = std::thread::hardware_concurrency();
+    struct part {
+        ValueType *dst;
+        const ValueType *src;
+        uint64_t count;
+    };
+    std::vector<part> parts;  // up to 8 per unit, 16 in total
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
-        const IndexType rows = m->row_end - m->row_begin;
-        if (!rows)
-            continue;
-        check(hipSetDevice(m->device), "hipSetDevice");
-        check(hipStreamSynchronize(unit_stream(u)), "y copy");
-        tr("spmv_hw: D2H done", ra_s);
-        ValueType *dst = y_fpga->values + m->row_begin;
-        const ValueType *src = m->h_stage;
-        const int T = rows < (1u << 20) ? 1 : (int)std::min(8u, hc ? hc : 1u);
-        auto add = [&](int t) {
-            const uint64_t b = uint64_t(rows) * t / T, e = uint64_t(rows) * (t + 1) / T;
-            for (uint64_t i = b; i < e; ++i)
-                dst[i] += src[i];
-        };
-        if (T == 1) {
-            add(0);
-        } else {
-            std::vector<std::thread> th;
-            for (int t = 0; t < T; ++t)
-                th.emplace_back(add, t);
-            for (auto &t : th)
-                t.join();
+        const uint64_t rows = m->row_end - m->row_begin;
+        const uint64_t T = rows < (1u << 18) ? 1 : std::min(8, std::max(1, 16 / units));
+        for (uint64_t t = 0; t < T && rows; ++t) {
+            const uint64_t b = rows * t / T, e = rows * (t + 1) / T;
+            parts.push_back({y_fpga->values + m->row_begin + b, m->h_stage + b, e - b});
         }
     }
+    std::atomic<bool> landed{false};
+    const char *pf_env = std::getenv("SPMV_HW_PREFAULT");
+    const bool pf = !(pf_env && pf_env[0] == '0');  // 0: let the adds take the page faults
+    auto work = [&](const part &q, bool wait) {
+        if (pf)
+            prefault(q.dst, q.count);
+        while (wait && !landed.load(std::memory_order_acquire))
+            std::this_thread::yield();
+        for (uint64_t i = 0; i < q.count; ++i)
+            q.dst[i] += q.src[i];
+    };
+    std::vector<std::thread> th;
+    for (size_t k = 1; k < parts.size(); ++k)
+        th.emplace_back(work, std::cref(parts[k]), true);
+    if (pf && !parts.empty())
+        prefault(parts[0].dst, parts[0].count);
+    for (int u = 0; u < units; ++u) {
+        if (impl(hw_matrix[u])->row_end == impl(hw_matrix[u])->row_begin)
+            continue;
+        check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
+        check(hipStreamSynchronize(unit_stream(u)), "y copy");
+    }
+    tr("spmv_hw: D2H done", ra_s);
+    landed.store(true, std::memory_order_release);
+    if (!parts.empty())
+        work(parts[0], false);
+    for (auto &t : th)
+        t.join();
     tr("spmv_hw: host accumulation", ra_s);
     const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
     std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
@@ -373,6 +412,7 @@ void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix)
             if (m->h_stage)
                 (void)hipHostFree(m->h_stage);
         }
+
         delete m;
     }
     std::free(hw_matrix);
