@@ -822,3 +822,38 @@ def test_slices_clustered_offsets(torch, monkeypatch, dtype):
             ys.append(y)
         assert np.array_equal(ys[0].view(np.uint8), ys[1].view(np.uint8))
         check(row_ptr, cols, val, x, oracle.spmv_gold(row_ptr, cols, val, x), ys[0], dtype)
+
+
+@pytest.mark.parametrize("units", [1, 3])
+@pytest.mark.parametrize("prefault", ["1", "0"])
+def test_spmv_hw_adds_into_nonzero_y_fpga(torch, monkeypatch, units, prefault):
+    """spmv_hw is `y_fpga += A x` (csr_hw.cpp:1555): on a 600K-row matrix (the threaded
+    accumulation, with and without mapping y's pages first, SPMV_HW_PREFAULT) a y_fpga holding
+    nonzero values gets exactly y0 + (A x) — the same device sums added on the host — and
+    the rows past the matrix (y_fpga longer than the matrix) are not touched."""
+    monkeypatch.setenv("SPMV_NGPUS", str(units))
+    monkeypatch.setenv("SPMV_HW_PREFAULT", prefault)
+    lib = spmv_hw.load(np.float64)
+    rng = np.random.default_rng(5)
+    n, w = 600_000, 16
+    rp = (np.arange(n + 1, dtype=np.int64) * w).astype(np.uint32)
+    start = np.clip(np.arange(n) - w // 2, 0, n - w)
+    col = (start[:, None] + np.arange(w)[None, :]).ravel().astype(np.uint32)
+    val = rng.uniform(-1, 1, n * w)
+    x = rng.uniform(0, 1, n)
+    m = lib.make_csr_matrix(rp, col, val, n)
+    hw, bm = lib.create_csr_hw_matrix(m)
+    hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(x), hw[0].contents.blocks, hw[0].contents.nr_cols)
+    ya = lib.make_csr_vector(np.zeros(n))
+    lib.spmv_hw(hw, hx, ya, bm)
+    y_ax = np.ctypeslib.as_array(ya.values, (n,)).copy()
+    y0 = rng.uniform(-10, 10, n + 1000)
+    yv = lib.make_csr_vector(y0.copy())
+    lib.spmv_hw(hw, hx, yv, bm)
+    got = np.ctypeslib.as_array(yv.values, (n + 1000,))
+    assert np.array_equal(got[:n], y0[:n] + y_ax)
+    assert np.array_equal(got[n:], y0[n:])
+    check(rp, col, val, x, oracle.spmv_gold(rp, col, val, x), y_ax, np.float64)
+    lib.delete_csr_hw_matrix(hw)
+    lib.free_bitmap(bm)
+    lib.delete_csr_hw_x_vector(hx)
