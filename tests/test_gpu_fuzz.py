@@ -102,7 +102,9 @@ def test_fuzz(torch, monkeypatch, seed, kern, dtype):
         assert st["kernel"] in (0, 2, 5)
     else:
         assert st["kernel"] == KERNEL_ID[kern.split("_")[0]]
-    if kern == "gold":
+    if kern == "gold" or (kern.startswith("slices") and dtype == np.float64):
+        # kernel 5 adds each row's products in CSR order from +0.0 with separate multiplies and
+        # adds (no v_fma_f64 in its fp64 ISA): bit for bit spmv_gold's arithmetic
         _bitwise(y, oracle.spmv_gold(row_ptr, col, val, x))
     elif kern in ("fpga", "blocked"):
         _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, m, block, vf))
