@@ -75,8 +75,11 @@ struct SliceOff<4> {  // absolute 32-bit columns (sbase = 0), when a slot spans 
 
 // PU pairs of slots per iteration; every load of the iteration is issued before the first
 // gather (pairs past the slice's end re-read its first pair and add nothing; TAIL: they are
-// skipped by a wave-uniform branch instead)
-template <typename V, int OB, int PU, bool TAIL = false>
+// skipped by a wave-uniform branch instead). A: the row accumulator, fp64 by default; A = V for
+// an fp32 matrix (env SPMV_SLICE_ACC=32) sums like spmv_gold in fp32. Each row's products are
+// added in CSR order from +0, and the select between each multiply and its add keeps them
+// apart (no fused multiply-add in the ISA), so y is bit for bit spmv_gold's when A == V.
+template <typename V, int OB, int PU, bool TAIL = false, typename A = double>
 __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restrict__ val, const void *__restrict__ offv,
                                                              const uint32_t *__restrict__ sbase,
                                                              const uint32_t *__restrict__ slot_off,
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restri
     const uint32_t L = __builtin_amdgcn_readfirstlane(slot_off[s + 1]) - j0;
     const uint32_t mylen = row < nrows ? len[row] : 0u;
     const uint32_t npairs = L / 2;
-    double acc = 0.0;
+    A acc = A(0);
     for (uint32_t p = 0; p < npairs; p += PU) {
         VT v[PU];
         OT o[PU];
@@ -137,10 +140,10 @@ __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restri
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
             const uint32_t j = 2 * (p + u);  // slot of the pair's first entry
-            const double t0 = double(v[u].x) * double(xv0[u]);
-            const double t1 = double(v[u].y) * double(xv1[u]);
-            acc += (p + u < npairs && j < mylen) ? t0 : 0.0;
-            acc += (p + u < npairs && j + 1 < mylen) ? t1 : 0.0;
+            const A t0 = A(v[u].x) * A(xv0[u]);
+            const A t1 = A(v[u].y) * A(xv1[u]);
+            acc += (p + u < npairs && j < mylen) ? t0 : A(0);
+            acc += (p + u < npairs && j + 1 < mylen) ? t1 : A(0);
         }
     }
     if (L & 1) {  // odd last slot, stored plainly
@@ -156,8 +159,8 @@ __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restri
             b = sbase[j0 + L - 1];
         }
         const V xv = x[b + (OB == 3 ? (o & 0x3FFFu) : (uint32_t)o)];
-        const double t = double(v) * double(xv);
-        acc += (L - 1 < mylen) ? t : 0.0;
+        const A t = A(v) * A(xv);
+        acc += (L - 1 < mylen) ? t : A(0);
     }
     if (row < nrows)
         y[row] = V(acc);
@@ -187,6 +190,24 @@ hipError_t launch_slices(const spmv_plan &p, const ValueType *d_x, ValueType *d_
         else                                                                                                     \
             SLV(OB, 4, true);                                                                                    \
     } while (0)
+    if constexpr (sizeof(ValueType) == 4) {
+        if (p.slice_acc_native) {  // fp32 accumulator (default variant only)
+#define SLF(OB)                                                                                                  \
+    launch_or_warm(warm, k_spmv_slices<ValueType, OB, 4, true, ValueType>, grid, dim3(kSliceThreads), 0, s,       \
+                   (const ValueType *)p.d_val, (const void *)p.d_colnar, (const uint32_t *)p.d_sbase,             \
+                   (const uint32_t *)p.d_slot_off, (const uint32_t *)p.d_slice_len, d_x, d_y, p.nr_rows, nsl)
+            if (p.slice_off_bytes == 1)
+                SLF(1);
+            else if (p.slice_off_bytes == 2 && p.slice_clustered)
+                SLF(3);
+            else if (p.slice_off_bytes == 2)
+                SLF(2);
+            else
+                SLF(4);
+#undef SLF
+            return hipGetLastError();
+        }
+    }
     if (p.slice_off_bytes == 1)
         SL(1);
     else if (p.slice_off_bytes == 2 && p.slice_clustered)
@@ -410,6 +431,11 @@ int build_slices(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         SPMV_TRY(hipGetLastError());
         SPMV_TRY(hipMemcpyAsync(&span, tspan.q, 4, hipMemcpyDeviceToHost, s));
         SPMV_TRY(hipStreamSynchronize(s));
+    }
+    // env SPMV_SLICE_ACC=32 (fp32 library): fp32 row accumulator, bitwise spmv_gold in fp32
+    {
+        const char *aenv = std::getenv("SPMV_SLICE_ACC");
+        p.slice_acc_native = sizeof(ValueType) == 4 && aenv && std::atoi(aenv) == 32;
     }
     // env SPMV_SLICE_NARROW=0 keeps 32-bit columns
     const char *nenv = std::getenv("SPMV_SLICE_NARROW");

@@ -105,6 +105,7 @@ struct spmv_plan {
     uint64_t nslices = 0, slice_slots = 0;
     int slice_off_bytes = 4;          // 1, 2 (offsets from the slot base) or 4 (absolute columns)
     bool slice_clustered = false;     // 2-byte offsets as (cluster << 14) | offset, 4 bases per slot
+    bool slice_acc_native = false;    // fp32 library: accumulate in fp32 (env SPMV_SLICE_ACC=32)
     double slice_pad_limit = 0.0;     // automatic choice: give up when stored / real entries exceeds it
 
     // panel-sweep representation (kernel 2, sweep.hip)

@@ -17,10 +17,10 @@ from test_gpu_parity import KERNEL_ID, _bitwise, check, run_device
 pytestmark = pytest.mark.gpu
 
 SEEDS = list(range(48))
-FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "gold", "slices", "slices_wide",
+FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "gold", "slices", "slices_wide", "slices_acc32",
                 "fpga", "blocked", "auto", "tune"]
 ENV = {"tiles_wide": {"SPMV_TILE_NARROW": "0"}, "sweep_unpacked": {"SPMV_SWEEP_PACKED": "0"},
-       "slices_wide": {"SPMV_SLICE_NARROW": "0"}}
+       "slices_wide": {"SPMV_SLICE_NARROW": "0"}, "slices_acc32": {"SPMV_SLICE_ACC": "32"}}
 
 
 @pytest.fixture(scope="module")
@@ -102,9 +102,10 @@ def test_fuzz(torch, monkeypatch, seed, kern, dtype):
         assert st["kernel"] in (0, 2, 5)
     else:
         assert st["kernel"] == KERNEL_ID[kern.split("_")[0]]
-    if kern == "gold" or (kern.startswith("slices") and dtype == np.float64):
-        # kernel 5 adds each row's products in CSR order from +0.0 with separate multiplies and
-        # adds (no v_fma_f64 in its fp64 ISA): bit for bit spmv_gold's arithmetic
+    if kern == "gold" or (kern.startswith("slices") and (dtype == np.float64 or kern == "slices_acc32")):
+        # kernel 5 adds each row's products in CSR order from +0 with separate multiplies and
+        # adds (no fused multiply-add in its ISA): bit for bit spmv_gold's arithmetic in fp64,
+        # and in fp32 with the fp32 accumulator (SPMV_SLICE_ACC=32)
         _bitwise(y, oracle.spmv_gold(row_ptr, col, val, x))
     elif kern in ("fpga", "blocked"):
         _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, m, block, vf))
