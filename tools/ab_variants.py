@@ -94,6 +94,9 @@ def main():
                 if kern.endswith("F32"):  # sweep with the fp32 (CAS) LDS accumulator for fp32 matrices
                     kern = kern[:-3]
                     os.environ["SPMV_SWEEP_ACC"] = "32"
+                if kern.endswith("A32"):  # slices with the fp32 row accumulator (fp32 matrices)
+                    kern = kern[:-3]
+                    os.environ["SPMV_SLICE_ACC"] = "32"
                 if kern.startswith("blocked") and kern[7:].isdigit():  # blockedW: W-column blocks
                     os.environ["SPMV_FPGA_BLOCK"] = kern[7:]
                     kern = "blocked"
@@ -109,6 +112,7 @@ def main():
                 os.environ.pop("SPMV_TILE_XCD", None)
                 os.environ.pop("SPMV_FPGA_BLOCK", None)
                 os.environ.pop("SPMV_SWEEP_ACC", None)
+                os.environ.pop("SPMV_SLICE_ACC", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
