@@ -82,7 +82,8 @@ typedef struct spmv_plan_stats {
                                     sweep, 3 = the reference FPGA path's order for env
                                     SPMV_FPGA_VF / SPMV_FPGA_BLOCK (bitwise), 4 = the same order
                                     by the reference's column-blocked dataflow (x blocks in LDS),
-                                    5 = slices (wave per 64 rows, slot-major).
+                                    5 = slices (wave per 64 rows, slot-major; DESIGN.md §3-4;
+                                    fp64: bitwise spmv_gold; fp32 too with env SPMV_SLICE_ACC=32).
                                     Chosen automatically (0, 2 or 5), or by env SPMV_HW_KERNEL =
                                     tiles | gold | sweep | fpga | blocked | slices | tune (build
                                     tiles, sweep and slices, time them on the matrix, keep the
