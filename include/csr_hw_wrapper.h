@@ -53,13 +53,22 @@ void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix);
 void delete_csr_hw_y_vector(csr_hw_vector **hw_vector);
 void delete_csr_hw_x_vector(csr_hw_vector *hw_vector);
 ValueType storage_overhead(csr_hw_matrix *matrix);
-int verification(IndexType nr_values, ValueType *sw_values, ValueType *hw_values, int verbose);
+/* nr_values is a plain 32-bit count at the C-ABI (the reference's IndexType is ap_uint<32>, the
+ * same 4 bytes; a caller-typed overload follows below for SPMV_USE_CALLER_CSR_TYPES builds) */
+int verification(uint32_t nr_values, ValueType *sw_values, ValueType *hw_values, int verbose);
 
 /* ---------------- Part 2: extensions ---------------- */
 
-/* Number of units ("ComputeUnits"): env SPMV_NGPUS (default 1). Unit u runs on HIP device
- * (u % device_count); more units than devices gives virtual units sharing a GPU. */
+/* Number of units ("ComputeUnits"): the last spmv_hw_set_units() value, else env SPMV_NGPUS
+ * (default 1). Unit u runs on HIP device (u % device_count); more units than devices gives
+ * virtual units sharing a GPU. create_csr_hw_matrix's *hw_matrix always holds at least 12 + 1
+ * slots (the reference's largest CU build, util.h:41-59) with the unused ones NULL, so a loop
+ * over a compile-time ComputeUnits (main.cpp:86-87) never reads past the array. */
 int spmv_hw_units(void);
+/* Set the unit count from the caller's compile-time CU (include/dropin/csr_hw_wrapper.h does
+ * this before main() when util.h defines ComputeUnits); 0 returns to env SPMV_NGPUS. Returns the
+ * previous setting. */
+int spmv_hw_set_units(int units);
 /* Bytes of sizeof(ValueType) this library was built for (8 = DOUBLE=1, 4 = DOUBLE=0). */
 int spmv_hw_value_bytes(void);
 /* Last error message of a Part-2 call on this thread ("" if none). */
@@ -171,6 +180,13 @@ void spmv_free_csr(csr_matrix *matrix);
 
 #ifdef __cplusplus
 }
+#if defined(SPMV_USE_CALLER_CSR_TYPES)
+/* the caller's IndexType may be a class (ap_uint<32>): pass it to the C-ABI as its 32-bit value */
+inline int verification(IndexType nr_values, ValueType *sw_values, ValueType *hw_values, int verbose)
+{
+    return verification((uint32_t)nr_values, sw_values, hw_values, verbose);
+}
+#endif
 #endif
 
 #endif /* CSR_HW_WRAPPER_H */

@@ -190,6 +190,19 @@ void oracle_spmv_fpga_order(IndexType nr_rows, IndexType nr_cols, const IndexTyp
     }
 }
 
+/* Test metric only (not in the reference): (|A||x|)_i in fp64, the denominator of the parity
+ * tests' componentwise-scaled error. */
+void oracle_abs_spmv(IndexType nr_rows, const IndexType *row_ptr, const IndexType *col_ind,
+                     const ValueType *values, const ValueType *x, double *out)
+{
+    for (IndexType i = 0; i < nr_rows; i++) {
+        double acc = 0.0;
+        for (IndexType j = row_ptr[i]; j < row_ptr[i + 1]; j++)
+            acc += fabs((double)values[j]) * fabs((double)x[col_ind[j]]);
+        out[i] = acc;
+    }
+}
+
 /* csr_hw.cpp:1571-1590: error when |sw - hw| >= 1e-5 or NaN. Returns the error count. */
 long oracle_verification_errors(IndexType n, const ValueType *sw, const ValueType *hw)
 {

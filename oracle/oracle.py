@@ -47,6 +47,8 @@ def lib(dtype=np.float64) -> ctypes.CDLL:
     L.oracle_spmv_fpga_order.argtypes = [u32, u32, _u32p, _u32p, vp, vp, vp, u32, ctypes.c_int]
     L.oracle_verification_errors.argtypes = [u32, vp, vp]
     L.oracle_verification_errors.restype = ctypes.c_long
+    L.oracle_abs_spmv.argtypes = [u32, _u32p, _u32p, vp, vp,
+                                  np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]
     assert L.oracle_value_bytes() == dtype.itemsize
     _LIBS[key] = L
     return L
@@ -118,9 +120,12 @@ def scaled_error(row_ptr, col, val, x, y_ref, y_test) -> float:
     (|A||x|)_i == 0 must match exactly)."""
     n = len(row_ptr) - 1
     absax = np.zeros(n, np.float64)
-    lens = np.diff(row_ptr.astype(np.int64))
-    rows = np.repeat(np.arange(n), lens)
-    np.add.at(absax, rows, np.abs(val.astype(np.float64)) * np.abs(x.astype(np.float64)[col]))
+    if n and len(col) and int(np.max(col)) >= len(x):
+        raise IndexError("scaled_error: column index past the end of x")
+    if n:
+        dtype = np.dtype(val.dtype)
+        lib(dtype).oracle_abs_spmv(n, _c(row_ptr, np.uint32), _c(col, np.uint32), _c(val, dtype),
+                                   _c(x, dtype), absax)
     diff = np.abs(y_ref.astype(np.float64) - y_test.astype(np.float64))
     zero = absax == 0
     if np.any(diff[zero] != 0) or np.any(np.isnan(diff)):

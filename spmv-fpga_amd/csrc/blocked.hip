@@ -210,12 +210,14 @@ hipError_t launch_blocked(const spmv_plan &p, const ValueType *d_x, ValueType *d
                    (const uint16_t *)p.d_colnar, (const uint32_t *)p.d_kptr, (const uint32_t *)p.d_kpos,           \
                    (const uint32_t *)p.d_unit_panel, (const uint32_t *)p.d_unit_ent, d_x, p.nr_cols, p.fpga_width,  \
                    p.d_bpart)
-        if (p.variant == 1) {  // measurement-only ablation: partials stored in compact-row order
+#ifdef SPMV_ABLATIONS
+        if (p.variant == 1) {  // measurement-only ablation (tools library only): partials stored in compact-row order
             launch_or_warm(warm, k_blocked_partials<ValueType, 1, true, 1>, dim3((unsigned)p.nunits),
                            dim3(kBlockedThreads), lds, s, (const ValueType *)p.d_val, (const uint16_t *)p.d_colnar,
                            (const uint32_t *)p.d_kptr, (const uint32_t *)p.d_kpos, (const uint32_t *)p.d_unit_panel,
                            (const uint32_t *)p.d_unit_ent, d_x, p.nr_cols, p.fpga_width, p.d_bpart);
         } else
+#endif
         switch (p.fpga_vf) {
         case 8: BK(8); break;
         case 4: BK(4); break;

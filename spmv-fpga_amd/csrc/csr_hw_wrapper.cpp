@@ -138,8 +138,25 @@ uint64_t ceil16(uint64_t bytes) { return (bytes + 15) / 16; }
 
 extern "C" {
 
+namespace {
+std::atomic<int> g_units_hint{0};  // spmv_hw_set_units (the caller's compile-time ComputeUnits)
+// the reference's largest build (CU=12, util.h:41-59): hw_matrix always has at least this many
+// slots, so a caller that loops its compile-time ComputeUnits (main.cpp:86-87) over fewer units
+// reads null handles (storage_overhead(NULL) = 0), never past the array
+constexpr int kMaxReferenceUnits = 12;
+}  // namespace
+
+int spmv_hw_set_units(int units)
+{
+    const int prev = g_units_hint.exchange(units > 0 ? units : 0);
+    return prev;
+}
+
 int spmv_hw_units(void)
 {
+    const int hint = g_units_hint.load();
+    if (hint > 0)
+        return hint;
     const char *s = std::getenv("SPMV_NGPUS");
     int u = s ? std::atoi(s) : 1;
     return u < 1 ? 1 : u;
@@ -161,7 +178,8 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
     if (spmv_partition_rows(matrix->row_ptr, n, units, bounds.data()))
         die(spmv_hw_last_error());
 
-    *hw_matrix = (csr_hw_matrix **)std::calloc(units + 1, sizeof(csr_hw_matrix *));
+    // null-terminated, and never shorter than the reference's largest CU count (+1)
+    *hw_matrix = (csr_hw_matrix **)std::calloc(std::max(units, kMaxReferenceUnits) + 1, sizeof(csr_hw_matrix *));
     uint64_t in_bytes = 0, nnz_total = 0;
     for (int u = 0; u < units; ++u) {
         auto *h = new hw_matrix_impl();
@@ -186,13 +204,19 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         spmv_plan_get_stats(h->plan, &st);
         const spmv_plan &pl = *h->plan;
         const bool sweep = pl.kernel == kKernelSweep;
-        // stored entries of the representation (padded for tiles and sweep, plain for gold)
-        const uint64_t stored = sweep ? pl.ent_pad : pl.kernel != kKernelTiles ? pl.nnz : pl.nnz_pad;
+        const bool slices = pl.kernel == kKernelSlices;
+        // stored entries of the representation (padded for tiles, sweep and slices, plain for
+        // gold / FPGA order / blocked)
+        const uint64_t stored = sweep    ? pl.ent_pad
+                                : slices ? pl.slice_slots * kWave
+                                : pl.kernel != kKernelTiles ? pl.nnz
+                                                            : pl.nnz_pad;
         const uint64_t val_bytes = stored * sizeof(ValueType);
         // the index stream of the unit's representation (opaque device address)
         h->sub[0] = sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)
-                    : pl.tile_col_bytes < 4 ? reinterpret_cast<BusDataType *>(pl.d_colnar)
-                                     : reinterpret_cast<BusDataType *>(pl.d_col);
+                    : (slices || pl.kernel == kKernelBlocked || pl.tile_col_bytes < 4)
+                        ? reinterpret_cast<BusDataType *>(pl.d_colnar)
+                        : reinterpret_cast<BusDataType *>(pl.d_col);
         h->nr_rows[0] = (IndexType)st.nr_nonempty_rows;
         h->nr_cols[0] = matrix->nr_cols;
         h->nr_nzeros[0] = (IndexType)stored;
@@ -236,7 +260,7 @@ void create_csr_hw_y_vector(csr_hw_matrix **hw_matrix, csr_hw_vector ***hw_vecto
     if (!hw_matrix || !hw_vector)
         die("create_csr_hw_y_vector: null argument");
     const int units = units_of(hw_matrix);
-    *hw_vector = (csr_hw_vector **)std::calloc(units + 1, sizeof(csr_hw_vector *));
+    *hw_vector = (csr_hw_vector **)std::calloc(std::max(units, kMaxReferenceUnits) + 1, sizeof(csr_hw_vector *));
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
         auto *v = new hw_vector_impl();
@@ -458,7 +482,7 @@ ValueType storage_overhead(csr_hw_matrix *matrix)
 }
 
 // csr_hw.cpp:1571-1590
-int verification(IndexType nr_values, ValueType *sw_values, ValueType *hw_values, int verbose)
+int verification(uint32_t nr_values, ValueType *sw_values, ValueType *hw_values, int verbose)
 {
     const ValueType diff_thres = (ValueType)1e-5;
     int status = 0;

@@ -829,10 +829,24 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
         set_error("spmv_plan_set_variant: bad arguments");
         return 1;
     }
+#ifndef SPMV_ABLATIONS
+    // the measurement-only ablations (some give a wrong y by design) exist only in the tools
+    // library built with -DSPMV_ABLATIONS (Makefile target `ablations`, tools/ab_variants.py)
+    if ((p->kernel == kKernelSweep && variant >= 54) || (p->kernel == kKernelBlocked && variant == 1)) {
+        set_error("spmv_plan_set_variant: measurement-only ablation variant (tools library only)");
+        return 1;
+    }
+#endif
     if (p->kernel == kKernelSweep)
         p->sweep_variant = variant;
     else
         p->variant = variant & 3;
+    // a graph captured with the previous variant must not be replayed
+    if (p->gexec) {
+        (void)hipSetDevice(p->device);
+        (void)hipGraphExecDestroy(p->gexec);
+        p->gexec = nullptr;
+    }
     return 0;
 }
 

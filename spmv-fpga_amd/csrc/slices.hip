@@ -86,6 +86,9 @@ __global__ __launch_bounds__(kSliceThreads) void k_spmv_slices(const V *__restri
                                                              const uint32_t *__restrict__ len, const V *__restrict__ x,
                                                              V *__restrict__ y, uint32_t nrows, uint32_t nslices)
 {
+    // separate multiply and add (no contraction to fma): the fp64 row sums are bitwise spmv_gold
+    // (csr.cpp:184-194), as in gold.hip and blocked.hip
+#pragma clang fp contract(off)
     typedef typename SliceVec<V>::T VT;
     typedef typename SliceOff<OB>::S OS;
     typedef typename SliceOff<OB>::T OT;

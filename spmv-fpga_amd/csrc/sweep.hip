@@ -522,7 +522,9 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 32: PK(1, 2); break;
         case 33: PK(1, 4); break;
         case 34: PK(2, 3); break;
-        // measurement-only ablations (54, 55, 60-63 give wrong y by design), DESIGN.md §4
+#ifdef SPMV_ABLATIONS
+        // measurement-only ablations, built only into the tools library (Makefile target
+        // `ablations`); 54, 55 and 60-63 give a wrong y by design, DESIGN.md §4
         case 60: if (p.nr_cols >= 32768) { PKA(1); } else { PK(2, 2); } break;  // x gathers all L2 hits
         case 61: PKA(2); break;  // no x gathers
         case 62: PKA(3); break;  // entries from L2 (first 4K of the unit), real gathers
@@ -533,6 +535,7 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 55: if (p.nr_cols >= 32768) { PKA(9); } else { PK(2, 2); } break;  // no LDS adds, all L2
         case 57: PKA(6); break;  // x gathers with the nt bit
         case 58: PKA(7); break;  // x gathers that bypass L1 (sc1)
+#endif
         default: PK(2, 2); break;
         }
 #undef PKA

@@ -30,7 +30,11 @@ IndexType = ctypes.c_uint32
 
 
 def lib_path(dtype=np.float64) -> str:
+    """The product library; env SPMV_HW_ABLATIONS=1 selects the tools-only build with the
+    measurement-only kernel ablations (`make -C spmv-fpga_amd ablations`, tools/ab_variants.py)."""
     name = {8: "libspmv_hw_f64.so", 4: "libspmv_hw_f32.so"}[np.dtype(dtype).itemsize]
+    if os.environ.get("SPMV_HW_ABLATIONS") == "1":
+        return os.path.join(LIBDIR, "ablations", name)
     return os.path.join(LIBDIR, name)
 
 
@@ -93,7 +97,7 @@ EXPORTS = [
     "create_csr_hw_matrix", "create_csr_hw_y_vector", "create_csr_hw_x_vector", "spmv_hw",
     "delete_csr_hw_matrix", "delete_csr_hw_y_vector", "delete_csr_hw_x_vector",
     "storage_overhead", "verification",
-    "spmv_hw_units", "spmv_hw_value_bytes", "spmv_hw_last_error",
+    "spmv_hw_units", "spmv_hw_set_units", "spmv_hw_value_bytes", "spmv_hw_last_error",
     "spmv_plan_create_device", "spmv_plan_create_host", "spmv_plan_run", "spmv_plan_run_graph", "spmv_plan_get_stats",
     "spmv_plan_set_variant", "spmv_plan_set_timing", "spmv_plan_get_timing", "spmv_plan_destroy", "spmv_partition_rows",
     "spmv_gen_banded", "spmv_gen_powerlaw_row_ptr", "spmv_gen_fill", "spmv_gen_vector",
@@ -129,6 +133,7 @@ class Lib:
             "storage_overhead": (V, [PM]),
             "verification": (ctypes.c_int, [IndexType, ctypes.POINTER(V), ctypes.POINTER(V), ctypes.c_int]),
             "spmv_hw_units": (ctypes.c_int, []),
+            "spmv_hw_set_units": (ctypes.c_int, [ctypes.c_int]),
             "spmv_hw_value_bytes": (ctypes.c_int, []),
             "spmv_hw_last_error": (ctypes.c_char_p, []),
             "spmv_plan_create_device": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, IndexType, IndexType,
@@ -238,6 +243,10 @@ class Lib:
 
     def units(self) -> int:
         return int(self.L.spmv_hw_units())
+
+    def set_units(self, units: int) -> int:
+        """spmv_hw_set_units: the caller's compile-time ComputeUnits (0 = env SPMV_NGPUS)."""
+        return int(self.L.spmv_hw_set_units(int(units)))
 
     # ---- Part 3: fast reader (host only) ----
     def read_csr_header(self, path: str):

@@ -31,3 +31,28 @@ def test_run_elf_f32_passes(name):
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "Verification PASSED!" in out.stdout
+
+
+DROPIN = os.path.join(ROOT, "tests", "dropin")
+
+
+@pytest.mark.parametrize("name", ["small", "wide", "trail"])
+@pytest.mark.parametrize("exe,ngpus,units", [("dropin_cu4.elf", None, 4), ("dropin_cu4.elf", "1", 4),
+                                             ("dropin_cu12_nohint.elf", "2", 2),
+                                             ("dropin_cu12_nohint.elf", None, 1)])
+def test_dropin_main_runs_with_compile_time_units(name, exe, ngpus, units):
+    """the main.cpp-shaped caller built against include/dropin/ runs end to end.
+    CU=4 registers 4 units whatever SPMV_NGPUS says; CU=12 without the registration loops 12
+    hw_matrix slots over 1 or 2 real units and reads NULL handles (storage_overhead = 0) for the
+    rest, never past the array."""
+    env = {k: v for k, v in os.environ.items() if k != "SPMV_NGPUS"}
+    if ngpus:
+        env["SPMV_NGPUS"] = ngpus
+    out = subprocess.run([os.path.join(DROPIN, exe), os.path.join(GOLDEN, f"{name}.mtx")], capture_output=True,
+                         text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert f"library units {units}" in out.stdout
+    assert "Verification PASSED!" in out.stdout
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("storage_overhead over")][0]
+    assert f"{units} non-null handles" in line, line
+    assert float(line.split(": ")[1].split(" MB")[0]) > 0

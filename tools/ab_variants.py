@@ -50,6 +50,13 @@ def main():
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--nnz", type=int, default=None)
     a = ap.parse_args()
+    # measurement-only ablations live in the tools library only (spmv-fpga_amd Makefile target
+    # `ablations`); the product library refuses them
+    abl = any((v.split(":")[0].startswith("sweep") and int(v.split(":")[1]) >= 54)
+              or (v.split(":")[0].startswith("blocked") and v.split(":")[1] == "1")
+              for v in a.variants.split(",") if ":" in v)
+    if abl:
+        os.environ["SPMV_HW_ABLATIONS"] = "1"
     dtype = np.float64 if a.dtype == "f64" else np.float32
     lib = spmv_hw.load(dtype)
     variants = [v if ":" in v else f"tiles:{v}" for v in a.variants.split(",")]
