@@ -12,12 +12,16 @@ Workloads:
   banded   (config 2): n = m = 1,000,000, 16 nnz/row.
   --dtype f32 (config 5): the power-law matrix in fp32.
 Multi-GPU (--gpus N, one process per GPU, torch.distributed over RCCL):
-  --scaling weak (default): rank r owns its own 10M-row / 160M-nnz row partition of an
-      (N*10M) x 10M matrix; x replicated; no collective inside the timed step (SURVEY §8e rows
-      are independent); value = total nnz of all ranks * 2 / max-over-ranks time.
-  --scaling strong (config 4): the single 10M/160M matrix split in nnz-balanced row slices.
-  The y exchange (RCCL reduce of partials = accum_results semantics, and RCCL gather of the
-  disjoint slices) is timed separately and reported in "exchange".
+  --scaling strong (default for N > 1; config 4): the single 10M/160M matrix split into N
+      nnz-balanced row slices (csr_hw.cpp:459-468), x replicated; value = 2 * 160M / the
+      max-over-ranks time of one SpMV (compute-only: every rank's slice, no collective inside
+      the timed step). The y exchange (RCCL gather of the disjoint slices, RCCL reduce of
+      full-length partials = accum_results' +=, and the all-gather of the iterative form) is
+      timed separately in "exchange", with the end-to-end rate beside it.
+  --scaling weak: rank r owns its own 10M-row / 160M-nnz row partition of an (N*10M) x 10M
+      matrix; value = total nnz of all ranks * 2 / max-over-ranks time. A strong run reports the
+      weak measurement as the side field "weak_companion" (and a weak run the strong one as
+      "strong_companion").
 
 Extra JSON fields: roofline (dominant kernel of the plan: k_spmv_sweep_packed for the power-law
 matrix, k_spmv_tiles for the banded one; HIP events on its launch stream),
@@ -58,18 +62,24 @@ def parse():
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--nnz", type=int, default=None)
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="default: strong (config 4) when --gpus > 1, weak (= single GPU) otherwise")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
     ap.add_argument("--no-xtiles", action="store_true",
                     help="skip the LDS x-tile (kernel 4, blocked) measurement beside the headline")
     ap.add_argument("--no-strong-companion", action="store_true",
                     help="N > 1 weak runs: skip the config-4 strong-scaling companion measurement")
+    ap.add_argument("--no-weak-companion", action="store_true",
+                    help="N > 1 strong runs: skip the weak-scaling companion measurement")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the row-parallel CPU line (the box's CPU share is 16)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.scaling is None:
+        a.scaling = "strong" if a.gpus > 1 else "weak"
+    return a
 
 
 def setup_dist(args):
@@ -224,6 +234,37 @@ def lds_xtiles(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
            "device_bytes": st["device_bytes"], "max_rel_diff_vs_value_kernel": diff}
     plan.destroy()
     del y
+    torch.cuda.empty_cache()
+    return res
+
+
+def weak_companion(lib, args, world, rank, dev, stream):
+    """Beside a strong-scaling run: every rank's own 10M-row / 160M-nnz partition (the weak
+    workload), timed like the headline; value = total nnz of all ranks * 2 / max-over-ranks."""
+    import copy
+    a = copy.copy(args)
+    a.scaling = "weak"
+    rp, col, val, x, ncols, desc = build_workload(lib, a, world, rank)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, ncols, device=dev.index, stream=stream)
+    st = plan.stats()
+    del rp, col, val
+    y = torch.empty(st["nr_rows"], dtype=x.dtype, device=dev)
+    for _ in range(args.warmup):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    ms = spmv_dist.max_over_ranks((time.perf_counter() - t0) * 1e3 / args.steps, dev)
+    nnz_all = spmv_dist.sum_over_ranks([float(st["nr_nzeros"])], dev)[0]
+    res = {"n_gpus": world, "value": round(2.0 * nnz_all / (ms * 1e-3) / 1e9, 3), "unit": "GFLOP/s",
+           "ms_per_step": round(ms, 5), "scaling": "weak", "nnz_per_rank": st["nr_nzeros"],
+           "kernel": st["kernel"]}
+    plan.destroy()
+    del x, y
     torch.cuda.empty_cache()
     return res
 
@@ -463,11 +504,17 @@ def main():
         del xb
         res["y_bytes"] = n_total * y.element_size()
         res["e2e_gflops_with_gather"] = round(2.0 * nnz_all / ((ms + res["gather_ms"]) * 1e-3) / 1e9, 2)
+        res["e2e_gflops_with_reduce"] = round(2.0 * nnz_all / ((ms + res["reduce_ms"]) * 1e-3) / 1e9, 2)
+        res["e2e_gflops_with_allgather"] = round(2.0 * nnz_all / ((ms + res["allgather_ms"]) * 1e-3) / 1e9, 2)
+        res["backend"] = dist.get_backend()
         exchange = res
 
     strong = None
     if world > 1 and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
         strong = strong_companion(lib, args, world, rank, dev, stream)
+    weak = None
+    if world > 1 and args.scaling == "strong" and args.workload == "powerlaw" and not args.no_weak_companion:
+        weak = weak_companion(lib, args, world, rank, dev, stream)
 
     cpu = None
     parity = None
@@ -502,6 +549,7 @@ def main():
             "exchange": exchange,
             "graph": graph,
             "strong_companion": strong,
+            "weak_companion": weak,
             "lds_xtiles": xtiles,
             "host_copy": host,
             "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},

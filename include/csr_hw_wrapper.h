@@ -144,6 +144,31 @@ void spmv_plan_destroy(spmv_plan *plan);
  * reference's S1 rule, csr_hw.cpp:459, without the FPGA alignment rules S2/S3). Host only. */
 int spmv_partition_rows(const IndexType *row_ptr, IndexType nr_rows, int units, IndexType *bounds);
 
+/* ---------------- Part 4: one process, several GPUs, RCCL exchange ----------
+ * A spmv_mgpu splits a host CSR matrix into nnz-balanced row slices, one per device (the
+ * per-CU split of prepare_balanced_hw_matrix, csr_hw.cpp:459-468), builds a plan per device,
+ * replicates x by an RCCL broadcast (x per CU, spmv.cpp:280-294) and exchanges y over xGMI with
+ * RCCL instead of merging on the host (accum_results, csr_hw.cpp:1531-1565;
+ * csr_hw_wrapper.cpp:276-281). One RCCL clique (ncclCommInitAll) over `devices` (NULL = 0..ndev-1,
+ * each at most once); RCCL is loaded at run time (librccl.so.1). All calls are synchronous and
+ * return 0 on success (spmv_hw_last_error() otherwise). */
+typedef struct spmv_mgpu spmv_mgpu;
+#define SPMV_MGPU_GATHER 0    /* send/recv of the disjoint row slices into the root's y */
+#define SPMV_MGPU_REDUCE 1    /* ncclReduce(sum) of full-length partials: accum_results' += */
+#define SPMV_MGPU_ALLGATHER 2 /* every device's next x = this y (square matrices; iterative use) */
+int spmv_mgpu_create(spmv_mgpu **mg, int ndev, const int *devices, const csr_matrix *matrix);
+/* host x[nr_cols] -> device devices[0], then an RCCL broadcast to every device */
+int spmv_mgpu_set_x(spmv_mgpu *mg, const ValueType *h_x);
+/* the SpMV on every device, then the `exchange` (SPMV_MGPU_*) */
+int spmv_mgpu_run(spmv_mgpu *mg, int exchange);
+/* y[nr_rows] of the last run to host memory (pass the exchange form of that run) */
+int spmv_mgpu_get_y(spmv_mgpu *mg, ValueType *h_y, int exchange);
+/* last run: kernels (max over devices) and exchange time, ms (HIP events on each device) */
+int spmv_mgpu_get_timing(const spmv_mgpu *mg, double *compute_ms, double *exchange_ms);
+/* row slice and device of rank d */
+int spmv_mgpu_slice(const spmv_mgpu *mg, int d, IndexType *row_begin, IndexType *row_end, int *device);
+void spmv_mgpu_destroy(spmv_mgpu *mg);
+
 /* ---------------- synthetic inputs (bench/test infrastructure) ---------------- */
 /* Banded: n x n, `width` non-zeros per row, columns [clamp(i - width/2, 0, n - width), +width),
  * values U(-1,1) from splitmix64(seed). Writes d_row_ptr[n+1], d_col[n*width], d_val. */

@@ -102,7 +102,11 @@ EXPORTS = [
     "spmv_plan_set_variant", "spmv_plan_set_timing", "spmv_plan_get_timing", "spmv_plan_destroy", "spmv_partition_rows",
     "spmv_gen_banded", "spmv_gen_powerlaw_row_ptr", "spmv_gen_fill", "spmv_gen_vector",
     "spmv_read_csr_header", "spmv_read_csr_matrix", "spmv_read_csr", "spmv_free_csr",
+    "spmv_mgpu_create", "spmv_mgpu_set_x", "spmv_mgpu_run", "spmv_mgpu_get_y", "spmv_mgpu_get_timing",
+    "spmv_mgpu_slice", "spmv_mgpu_destroy",
 ]
+
+MGPU_GATHER, MGPU_REDUCE, MGPU_ALLGATHER = 0, 1, 2  # include/csr_hw_wrapper.h SPMV_MGPU_*
 
 
 class Lib:
@@ -159,6 +163,15 @@ class Lib:
             "spmv_read_csr_matrix": (ctypes.c_int, [ctypes.POINTER(self.csr_matrix), ctypes.c_char_p]),
             "spmv_read_csr": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(self.csr_matrix)]),
             "spmv_free_csr": (None, [ctypes.POINTER(self.csr_matrix)]),
+            "spmv_mgpu_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(self.csr_matrix)]),
+            "spmv_mgpu_set_x": (ctypes.c_int, [vp, ctypes.POINTER(V)]),
+            "spmv_mgpu_run": (ctypes.c_int, [vp, ctypes.c_int]),
+            "spmv_mgpu_get_y": (ctypes.c_int, [vp, ctypes.POINTER(V), ctypes.c_int]),
+            "spmv_mgpu_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                                    ctypes.POINTER(ctypes.c_double)]),
+            "spmv_mgpu_slice": (ctypes.c_int, [vp, ctypes.c_int, up, up, ctypes.POINTER(ctypes.c_int)]),
+            "spmv_mgpu_destroy": (None, [vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -349,6 +362,48 @@ class Plan:
             self.destroy()
         except Exception:
             pass
+
+
+class MultiGpu:
+    """Part 4 of the C-ABI (spmv_mgpu_*): one process, `ndev` GPUs, RCCL exchange of y."""
+
+    def __init__(self, lib: Lib, matrix, devices=None, ndev: int = None):
+        self.lib = lib
+        devs = list(devices) if devices is not None else list(range(ndev or 1))
+        arr = (ctypes.c_int * len(devs))(*devs)
+        h = ctypes.c_void_p()
+        lib._ok(lib.L.spmv_mgpu_create(ctypes.byref(h), len(devs), arr, ctypes.byref(matrix)), "spmv_mgpu_create")
+        self.h, self.ndev, self.nr_rows, self.nr_cols = h, len(devs), int(matrix.nr_rows), int(matrix.nr_cols)
+
+    def set_x(self, x) -> None:
+        x = np.ascontiguousarray(x, self.lib.dtype)
+        self.lib._ok(self.lib.L.spmv_mgpu_set_x(self.h, x.ctypes.data_as(ctypes.POINTER(self.lib.V))),
+                     "spmv_mgpu_set_x")
+
+    def run(self, exchange: int = MGPU_GATHER) -> None:
+        self.lib._ok(self.lib.L.spmv_mgpu_run(self.h, int(exchange)), "spmv_mgpu_run")
+
+    def y(self, exchange: int = MGPU_GATHER):
+        out = np.empty(self.nr_rows, self.lib.dtype)
+        self.lib._ok(self.lib.L.spmv_mgpu_get_y(self.h, out.ctypes.data_as(ctypes.POINTER(self.lib.V)),
+                                                int(exchange)), "spmv_mgpu_get_y")
+        return out
+
+    def timing(self):
+        c, e = ctypes.c_double(), ctypes.c_double()
+        self.lib._ok(self.lib.L.spmv_mgpu_get_timing(self.h, ctypes.byref(c), ctypes.byref(e)), "spmv_mgpu_get_timing")
+        return c.value, e.value
+
+    def slice(self, d: int):
+        b, e, dev = IndexType(), IndexType(), ctypes.c_int()
+        self.lib._ok(self.lib.L.spmv_mgpu_slice(self.h, d, ctypes.byref(b), ctypes.byref(e), ctypes.byref(dev)),
+                     "spmv_mgpu_slice")
+        return b.value, e.value, dev.value
+
+    def destroy(self) -> None:
+        if self.h:
+            self.lib.L.spmv_mgpu_destroy(self.h)
+            self.h = None
 
 
 def _stream_ptr(stream):

@@ -1,0 +1,94 @@
+"""Part 4 of the C-ABI (spmv_mgpu_*): one process drives the visible GPUs through one RCCL clique
+(ncclCommInitAll) -- nnz-balanced row slices per device (csr_hw.cpp:459-468), x replicated by an
+RCCL broadcast (spmv.cpp:280-294), y exchanged on the devices: send/recv gather of the slices,
+reduce of full-length partials (accum_results' +=, csr_hw.cpp:1531-1565) and the all-gather that
+makes y the next x. Runs with every GPU the box has (1 on the test box; the driver's 8-GPU node
+runs the same code with 8). y is checked against the oracle's spmv_gold (csr.cpp:184-194)."""
+import numpy as np
+import pytest
+
+import oracle
+import spmv_hw
+from conftest import GOLDEN, manifest
+
+pytestmark = pytest.mark.gpu
+
+TOL = {np.dtype(np.float64): 1e-12, np.dtype(np.float32): 2e-6}
+
+
+def _ndev():
+    import torch
+    return torch.cuda.device_count()
+
+
+def _powerlaw_host(lib, n, z):
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    return (rp.cpu().numpy().view(np.uint32), col.cpu().numpy().view(np.uint32), val.cpu().numpy(),
+            x.cpu().numpy())
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("exchange", [spmv_hw.MGPU_GATHER, spmv_hw.MGPU_REDUCE])
+def test_mgpu_gather_and_reduce_match_oracle(dtype, exchange):
+    lib = spmv_hw.load(dtype)
+    n, z = 300_000, 4_800_000
+    rp, col, val, x = _powerlaw_host(lib, n, z)
+    m = lib.make_csr_matrix(rp, col, val, n)
+    mg = spmv_hw.MultiGpu(lib, m, ndev=_ndev())
+    slices = [mg.slice(d) for d in range(mg.ndev)]
+    assert slices[0][0] == 0 and slices[-1][1] == n
+    assert all(slices[d][1] == slices[d + 1][0] for d in range(mg.ndev - 1))
+    mg.set_x(x)
+    ref = oracle.spmv_gold(rp, col, val, x)
+    for _ in range(2):  # the second run reuses the exchange buffers
+        mg.run(exchange)
+        y = mg.y(exchange)
+        assert oracle.scaled_error(rp, col, val, x, ref, y) <= TOL[np.dtype(dtype)]
+    c, e = mg.timing()
+    assert c > 0 and e >= 0
+    mg.destroy()
+
+
+def test_mgpu_allgather_iterates_y_into_x():
+    """Two all-gather runs compute A(Ax): the first y becomes every device's next x."""
+    lib = spmv_hw.load(np.float64)
+    n, z = 200_000, 3_200_000
+    rp, col, val, x = _powerlaw_host(lib, n, z)
+    m = lib.make_csr_matrix(rp, col, val, n)
+    mg = spmv_hw.MultiGpu(lib, m, ndev=_ndev())
+    mg.set_x(x)
+    mg.run(spmv_hw.MGPU_ALLGATHER)
+    y1 = mg.y(spmv_hw.MGPU_ALLGATHER)
+    ref1 = oracle.spmv_gold(rp, col, val, x)
+    assert oracle.scaled_error(rp, col, val, x, ref1, y1) <= 1e-12
+    mg.run(spmv_hw.MGPU_ALLGATHER)
+    y2 = mg.y(spmv_hw.MGPU_ALLGATHER)
+    ref2 = oracle.spmv_gold(rp, col, val, y1)
+    assert oracle.scaled_error(rp, col, val, y1, ref2, y2) <= 1e-12
+    mg.destroy()
+
+
+@pytest.mark.parametrize("name", sorted(manifest().keys()))
+def test_mgpu_on_golden_fixtures(name):
+    import os
+    lib = spmv_hw.load(np.float64)
+    _, c, rp, col, val, _ = oracle.read_csr(os.path.join(GOLDEN, manifest()[name]["file"]), np.float64)
+    x = np.load(os.path.join(GOLDEN, f"{name}.x.f64.npy"), allow_pickle=False)
+    y_gold = np.load(os.path.join(GOLDEN, f"{name}.y_gold.f64.npy"), allow_pickle=False)
+    mg = spmv_hw.MultiGpu(lib, lib.make_csr_matrix(rp, col, val, c), ndev=_ndev())
+    mg.set_x(x)
+    for ex in (spmv_hw.MGPU_GATHER, spmv_hw.MGPU_REDUCE):
+        mg.run(ex)
+        assert oracle.scaled_error(rp, col, val, x, y_gold, mg.y(ex)) <= 1e-12
+    mg.destroy()
+
+
+def test_mgpu_rejects_bad_devices():
+    lib = spmv_hw.load(np.float64)
+    rp = np.array([0, 1], np.uint32)
+    m = lib.make_csr_matrix(rp, np.zeros(1, np.uint32), np.ones(1), 1)
+    with pytest.raises(RuntimeError, match="does not exist"):
+        spmv_hw.MultiGpu(lib, m, devices=[_ndev()])
+    with pytest.raises(RuntimeError, match="appears twice"):
+        spmv_hw.MultiGpu(lib, m, devices=[0, 0])
