@@ -126,6 +126,8 @@ struct spmv_plan {
     uint32_t *d_s_cbase = nullptr;   // packed form: base column per 128-entry chunk
     bool sweep_packed = false;
     bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)
+    bool sweep_det = false;          // env SPMV_SWEEP_DETERMINISTIC=1: one segment per wave (sweep.hip)
+    uint32_t *d_seg_row = nullptr;   // deterministic form: row ranges of the wave segments [npanels * waves + 1]
     double locality = -1.0;    // probe result used by the automatic kernel choice
     double tuned_ms[3] = {-1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: measured tiles / sweep / slices ms
 

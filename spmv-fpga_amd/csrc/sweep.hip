@@ -83,6 +83,10 @@ __device__ __forceinline__ void lds_add_n(float *y, const uint32_t (&idx)[N], co
     }
 }
 
+// sentinel: the padding entries of the deterministic layout's segments (k_spmv_sweep_ordered
+// sends them to the panel's scratch slot)
+constexpr uint16_t kSweepPadRow = 0xFFFF;
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -350,16 +354,127 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
 }
 
-// chunk c of 128 entries: base = min column; fails the plan's packing when the span >= 65536
-__global__ void k_sweep_chunk_base(const uint32_t *__restrict__ col, uint64_t nchunks, uint32_t *__restrict__ cbase,
-                                   uint32_t *__restrict__ bad)
+// Deterministic form (env SPMV_SWEEP_DETERMINISTIC=1). The default kernel lets all 16 waves add
+// into any row of the panel, so a row's products land in timing order and y changes in its
+// last bits from run to run. Here each panel's rows are cut into T/64 nnz-balanced segments, one
+// per wave, and each segment has its own column-sorted, chunk-padded entries: a row's products
+// are added by its one wave, in the fixed order of its entries (the fixed-order accumulation of
+// compute_results, spmv.cpp:66-104, though not the same order), so y is the same bits on every
+// run. The waves still sweep the columns together (loose synchronisation, LAG iterations), but
+// each gather instruction covers 64 entries of one wave's rows only, so fewer lanes share an x
+// line than in the default form.
+// PK: packed entries (rc = row << 16 | column offset, one base per 32 entries); otherwise the
+// 14-byte form (s_col u32, s_row u16, value) of segments too sparse for 16-bit offsets.
+template <typename V, int T, int Q, int LAG, bool PK, typename A = double>
+__global__ __launch_bounds__(T) void k_spmv_sweep_ordered(
+    const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const uint16_t *__restrict__ srow16,
+    const V *__restrict__ val, const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ seg_row,
+    const uint32_t *__restrict__ seg_ent, const V *__restrict__ x, V *__restrict__ y)
+{
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    constexpr uint32_t W = T / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    A *ylds = reinterpret_cast<A *>(smem);
+    __shared__ uint32_t progress[W];
+    const uint32_t p = blockIdx.x;
+    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane2 = 2u * (threadIdx.x & 63);
+    const uint64_t e0 = seg_ent[p * W + wave], e1 = seg_ent[p * W + wave + 1];
+    const uint32_t roff = seg_row[p * W + wave] - r0;  // the wave's first row inside the panel
+    const bool hi_half = (threadIdx.x & 63) >= 32;
+    for (uint32_t i = threadIdx.x; i <= R; i += T)
+        ylds[i] = A(0);
+    if (threadIdx.x < W)
+        progress[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t iter = 0;
+    const uint64_t last_chunk = e1 > e0 ? e1 - 128 : e0;
+    for (uint64_t base = e0; base < e1; base += Q * 128ull) {
+        u32x2 w[Q];
+        uint32_t cb[Q][2];
+        V v[Q][2];
+        bool ok[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            uint64_t wbase = base + 128ull * q;  // this wave's own consecutive chunks
+            ok[q] = wbase < e1;                  // wave-uniform
+            wbase = ok[q] ? wbase : last_chunk;
+            const uint64_t e = wbase + lane2;
+            w[q] = lds_<true>(reinterpret_cast<const u32x2 *>(rc + e));
+            if constexpr (PK) {
+                // one base per 32 entries: gather instruction j covers logical entries 64j + lane,
+                // i.e. quarters 2j (lanes 0-31) and 2j + 1 (lanes 32-63); four scalar loads per chunk
+                const uint32_t *b4 = cbase + (wbase >> 5);
+                const uint32_t b0 = b4[0], b1 = b4[1], b2 = b4[2], b3 = b4[3];
+                cb[q][0] = hi_half ? b1 : b0;
+                cb[q][1] = hi_half ? b3 : b2;
+            } else {  // absolute columns in w, rows from s_row
+                const u16x2 r2 = lds_<true>(reinterpret_cast<const u16x2 *>(srow16 + e));
+                cb[q][0] = r2.x;
+                cb[q][1] = r2.y;
+            }
+            loadv<true, 2>(val, e, v[q]);
+        }
+        V xv[Q][2];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if constexpr (PK) {
+                xv[q][0] = x[cb[q][0] + (w[q].x & 0xFFFFu)];
+                xv[q][1] = x[cb[q][1] + (w[q].y & 0xFFFFu)];
+            } else {
+                xv[q][0] = x[w[q].x];
+                xv[q][1] = x[w[q].y];
+            }
+        }
+        uint32_t ri[2 * Q];
+        A pv[2 * Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t a = PK ? w[q].x >> 16 : cb[q][0], b = PK ? w[q].y >> 16 : cb[q][1];
+            ri[2 * q] = ok[q] && a != kSweepPadRow ? a + roff : R;
+            ri[2 * q + 1] = ok[q] && b != kSweepPadRow ? b + roff : R;
+            pv[2 * q] = A(v[q][0]) * A(xv[q][0]);
+            pv[2 * q + 1] = A(v[q][1]) * A(xv[q][1]);
+        }
+        lds_add_n<2 * Q>(ylds, ri, pv);
+        ++iter;
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_store(&progress[wave], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (;;) {  // wait while more than LAG iterations ahead of the slowest unfinished wave
+            const uint32_t lane = threadIdx.x & 63;
+            uint32_t pr = lane < W ? __hip_atomic_load(&progress[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                   : 0xFFFFFFFFu;
+#pragma unroll
+            for (int d = 1; d < (int)W; d <<= 1) {
+                const uint32_t o = __shfl_xor(pr, d, 64);
+                pr = o < pr ? o : pr;
+            }
+            if (__builtin_amdgcn_readfirstlane(pr) + LAG >= iter)
+                break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    // a finished wave never holds the others back
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store(&progress[wave], 0xFFFFFFFFu - LAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < R; i += T)
+        y[r0 + i] = V(ylds[i]);
+}
+
+// group c of G entries (a 128-entry chunk, or half a chunk = one gather instruction in the
+// deterministic form): base = min column; fails the plan's packing when the span >= 65536
+__global__ void k_sweep_chunk_base(const uint32_t *__restrict__ col, uint64_t nchunks, uint32_t G,
+                                   uint32_t *__restrict__ cbase, uint32_t *__restrict__ bad)
 {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchunks)
         return;
     uint32_t lo = 0xFFFFFFFFu, hi = 0;
-    for (int k = 0; k < 128; ++k) {
-        const uint32_t v = col[c * 128 + k];
+    for (uint32_t k = 0; k < G; ++k) {
+        const uint32_t v = col[c * G + k];
         lo = v < lo ? v : lo;
         hi = v > hi ? v : hi;
     }
@@ -368,14 +483,14 @@ __global__ void k_sweep_chunk_base(const uint32_t *__restrict__ col, uint64_t nc
         atomicOr(bad, 1u);
 }
 
-// in place: col[k] <- (row << 16) | (col - base)
+// in place: col[k] <- (row << 16) | (col - base of k's group of 2^gshift entries)
 __global__ void k_sweep_pack_rc(uint32_t *__restrict__ col, const uint16_t *__restrict__ row,
-                                const uint32_t *__restrict__ cbase, uint64_t n)
+                                const uint32_t *__restrict__ cbase, uint64_t n, uint32_t gshift)
 {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n)
         return;
-    col[k] = ((uint32_t)row[k] << 16) | (col[k] - cbase[k >> 7]);
+    col[k] = ((uint32_t)row[k] << 16) | (col[k] - cbase[k >> gshift]);
 }
 
 // Lane-order permutation inside each 128-entry chunk: memory word 2l+j holds logical entry
@@ -452,7 +567,8 @@ __global__ void k_sweep_scatter(const uint32_t *__restrict__ keys, const uint32_
 template <typename V>
 __global__ void k_sweep_pad(uint32_t npanels, const uint32_t *__restrict__ panel_row,
                             const uint32_t *__restrict__ off, const uint32_t *__restrict__ poff,
-                            uint32_t *__restrict__ s_col, uint16_t *__restrict__ s_row, V *__restrict__ s_val)
+                            uint32_t *__restrict__ s_col, uint16_t *__restrict__ s_row, V *__restrict__ s_val,
+                            bool sentinel)
 {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npanels)
@@ -462,7 +578,7 @@ __global__ void k_sweep_pad(uint32_t npanels, const uint32_t *__restrict__ panel
     const uint32_t pad_col = first_pad > poff[p] ? s_col[first_pad - 1] : 0u;
     for (uint64_t d = first_pad; d < poff[p + 1]; ++d) {
         s_col[d] = pad_col;  // value 0: adds nothing; column kept near the panel's last one
-        s_row[d] = (uint16_t)R;  // scratch slot, never written back
+        s_row[d] = sentinel ? kSweepPadRow : (uint16_t)R;  // scratch slot, never written back
         s_val[d] = V(0);
     }
 }
@@ -503,6 +619,17 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT, A>, grid, block, lds, s, p.d_s_col,   \
                        p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, d_x, d_y)
+    if (p.sweep_det) {  // deterministic form
+        if (p.sweep_packed)
+            launch_or_warm(warm, k_spmv_sweep_ordered<ValueType, T, 2, 2, true, A>, grid, block, lds, s, p.d_s_col,
+                           p.d_s_cbase, (const uint16_t *)nullptr, p.d_s_val, p.d_panel_row, p.d_seg_row,
+                           p.d_unit_ent, d_x, d_y);
+        else
+            launch_or_warm(warm, k_spmv_sweep_ordered<ValueType, T, 2, 2, false, A>, grid, block, lds, s, p.d_s_col,
+                           (const uint32_t *)nullptr, p.d_s_row, p.d_s_val, p.d_panel_row, p.d_seg_row,
+                           p.d_unit_ent, d_x, d_y);
+        return;
+    }
     if (p.sweep_packed) {
 #define PKN(NT, Q, LAG, ABL)                                                                        \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
@@ -614,7 +741,11 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     cus *= 1024 / p.sweep_threads;  // resident workgroups per round
     // env SPMV_SWEEP_SPLIT: 0 = never split, 2 = split whenever >= 2 pieces fit, else heuristic
     const char *senv = std::getenv("SPMV_SWEEP_SPLIT");
-    const bool allow_split = !(senv && senv[0] == '0');
+    // env SPMV_SWEEP_DETERMINISTIC=1: one segment of rows per wave (k_spmv_sweep_ordered); panels
+    // are never cut into column pieces in that form
+    const char *denv = std::getenv("SPMV_SWEEP_DETERMINISTIC");
+    const bool det = denv && denv[0] == '1';
+    const bool allow_split = !(senv && senv[0] == '0') && !det;
     const bool force_split = senv && senv[0] == '2';
     bool split_mode = false;
     std::vector<uint32_t> prow;
@@ -652,28 +783,50 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         }
     }
     const uint32_t P = (uint32_t)(prow.size() - 1);
-    std::vector<uint32_t> off(P + 1), poff(P + 1);
+    // sort segments: the panels, or (deterministic form) W nnz-balanced row segments per panel,
+    // each padded to whole chunks of its own
+    const uint32_t W = det ? (uint32_t)(p.sweep_threads / kWave) : 1;
+    std::vector<uint32_t> srow;
+    if (det) {
+        srow.assign(1, 0);
+        for (uint32_t q = 0; q < P; ++q) {
+            const uint64_t a = h_rp[prow[q]], b = h_rp[prow[q + 1]];
+            for (uint32_t w = 1; w < W; ++w) {
+                // the row boundary nearest to the segment's share of the panel's entries (keeps
+                // the segments' densities close: their 32-entry column groups must stay < 65536)
+                const IndexType target = (IndexType)(a + (b - a) * w / W);
+                IndexType r = (IndexType)(std::lower_bound(h_rp + prow[q], h_rp + prow[q + 1], target) - h_rp);
+                if (r > prow[q] && target - h_rp[r - 1] < h_rp[r] - target)
+                    --r;
+                r = std::min<IndexType>(std::max<IndexType>(r, srow.back()), prow[q + 1]);
+                srow.push_back(r);
+            }
+            srow.push_back(prow[q + 1]);
+        }
+    } else {
+        srow = prow;
+    }
+    const uint32_t S = (uint32_t)(srow.size() - 1);
+    std::vector<uint32_t> off(S + 1), poff(S + 1);
     off[0] = poff[0] = 0;
     uint32_t rmax_used = 0;
     uint64_t padded = 0;
-    for (uint32_t q = 0; q < P; ++q) {
-        const uint64_t cnt = uint64_t(h_rp[prow[q + 1]]) - h_rp[prow[q]];
+    for (uint32_t q = 0; q < S; ++q) {
+        const uint64_t cnt = uint64_t(h_rp[srow[q + 1]]) - h_rp[srow[q]];
         padded += (cnt + kSweepChunk - 1) / kSweepChunk * kSweepChunk;
         off[q + 1] = (uint32_t)(off[q] + cnt);
         poff[q + 1] = (uint32_t)padded;
-        rmax_used = std::max(rmax_used, prow[q + 1] - prow[q]);
     }
+    for (uint32_t q = 0; q < P; ++q)
+        rmax_used = std::max(rmax_used, prow[q + 1] - prow[q]);
     if (padded > 0xFFFFFFFFull) {  // panel_ent is u32: the padded layout must fit (nnz near 2^32)
         set_error("build_sweep: padded entry count exceeds 32 bits");
         return 2;
     }
-    if (nnz > 0x7FFFFFFFull) {  // hipcub's radix sort takes an int item count
-        set_error("build_sweep: more than 2^31-1 non-zeros in one slice");
-        return 2;
-    }
     p.npanels = P;
     p.panel_rmax = rmax_used;
-    p.ent_pad = poff[P];
+    p.ent_pad = poff[S];
+    p.sweep_det = det;
     // work units: pieces of whole chunks per panel. split mode: `split` pieces each; any panel
     // with more than twice the mean entry count (a panel holding very long rows) is cut
     // further, so that no workgroup gets more than ~2x the mean work
@@ -681,25 +834,32 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     const double mean = P ? double(padded) / P : 0.0;
     std::vector<uint32_t> punit(P + 1, 0);
     for (uint32_t q = 0; q < P; ++q) {
-        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
+        const uint64_t chunks = (uint64_t(poff[(q + 1) * W]) - poff[q * W]) / kSweepChunk;
         uint64_t k = split * std::max<uint64_t>(
                                  1, (uint64_t)std::ceil(double(poff[q + 1] - poff[q]) / std::max(2.0 * mean, 1.0)));
-        k = std::max<uint64_t>(1, std::min<uint64_t>(k, chunks));
+        k = det ? 1 : std::max<uint64_t>(1, std::min<uint64_t>(k, chunks));
         punit[q + 1] = punit[q] + (uint32_t)k;
     }
     const uint32_t U = punit[P];
-    std::vector<uint32_t> uent((size_t)U + 1), upanel(std::max<uint32_t>(U, 1));
+    std::vector<uint32_t> uent, upanel(std::max<uint32_t>(U, 1));
     bool multi = false;
-    for (uint32_t q = 0; q < P; ++q) {
-        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
-        const uint32_t k = punit[q + 1] - punit[q];
-        multi |= k > 1;
-        for (uint32_t t = 0; t < k; ++t) {
-            uent[punit[q] + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / k));
-            upanel[punit[q] + t] = q;
+    if (det) {
+        uent = poff;  // the deterministic kernel reads each wave's segment range
+        for (uint32_t q = 0; q < P; ++q)
+            upanel[q] = q;
+    } else {
+        uent.assign((size_t)U + 1, 0);
+        for (uint32_t q = 0; q < P; ++q) {
+            const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
+            const uint32_t k = punit[q + 1] - punit[q];
+            multi |= k > 1;
+            for (uint32_t t = 0; t < k; ++t) {
+                uent[punit[q] + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / k));
+                upanel[punit[q] + t] = q;
+            }
         }
+        uent[U] = poff[P];
     }
-    uent[U] = poff[P];
     p.sweep_split = multi ? std::max<uint32_t>(split, 2) : 1;  // > 1: combine kernel needed
     p.nunits = U;
     if (multi)
@@ -709,18 +869,25 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     SPMV_TRY(hipMemcpyAsync(p.d_unit_panel, upanel.data(), upanel.size() * 4, hipMemcpyHostToDevice, s));
     SPMV_TRY(hipMemcpyAsync(p.d_panel_unit, punit.data(), punit.size() * 4, hipMemcpyHostToDevice, s));
 
-    // bucket shift so that P * buckets fits 32-bit keys
+    // bucket shift so that S * buckets fits 32-bit keys
     uint32_t shift = 0;
-    while ((uint64_t(P) * ((uint64_t(p.nr_cols) >> shift) + 1)) >= (1ull << 32))
+    while ((uint64_t(S) * ((uint64_t(p.nr_cols) >> shift) + 1)) >= (1ull << 32))
         ++shift;
     const uint64_t nbuckets = (uint64_t(p.nr_cols) >> shift) + 1;
     int end_bit = 1;
-    while (end_bit < 32 && (1ull << end_bit) < uint64_t(P) * nbuckets)
+    while (end_bit < 32 && (1ull << end_bit) < uint64_t(S) * nbuckets)
         ++end_bit;
 
     SPMV_TRY(hipMalloc((void **)&p.d_panel_row, (P + 1) * 4));
     SPMV_TRY(hipMalloc((void **)&p.d_unit_ent, uent.size() * 4));
     SPMV_TRY(hipMemcpyAsync(p.d_panel_row, prow.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
+    // rows of the sort segments (the panels themselves unless deterministic)
+    uint32_t *d_srow = p.d_panel_row;
+    if (det) {
+        SPMV_TRY(hipMalloc((void **)&p.d_seg_row, (S + 1) * 4));
+        SPMV_TRY(hipMemcpyAsync(p.d_seg_row, srow.data(), (S + 1) * 4, hipMemcpyHostToDevice, s));
+        d_srow = p.d_seg_row;
+    }
     SPMV_TRY(hipMemcpyAsync(p.d_unit_ent, uent.data(), uent.size() * 4, hipMemcpyHostToDevice, s));
     SPMV_TRY(hipMalloc((void **)&p.d_s_col, std::max<uint64_t>(p.ent_pad, 4) * 4));
     SPMV_TRY(hipMalloc((void **)&p.d_s_row, std::max<uint64_t>(p.ent_pad, 4) * 2));
@@ -748,11 +915,11 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         if (e_ != hipSuccess)                  \
             return fail(e_, #x);               \
     } while (0)
-    SW_TRY(hipMalloc((void **)&d_off, (P + 1) * 4));
-    SW_TRY(hipMalloc((void **)&d_poff, (P + 1) * 4));
+    SW_TRY(hipMalloc((void **)&d_off, (S + 1) * 4));
+    SW_TRY(hipMalloc((void **)&d_poff, (S + 1) * 4));
     SW_TRY(hipMalloc((void **)&d_rp, (size_t(n) + 1) * 4));
-    SW_TRY(hipMemcpyAsync(d_off, off.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
-    SW_TRY(hipMemcpyAsync(d_poff, poff.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
+    SW_TRY(hipMemcpyAsync(d_off, off.data(), (S + 1) * 4, hipMemcpyHostToDevice, s));
+    SW_TRY(hipMemcpyAsync(d_poff, poff.data(), (S + 1) * 4, hipMemcpyHostToDevice, s));
     SW_TRY(hipMemcpyAsync(d_rp, h_rp, (size_t(n) + 1) * 4, hipMemcpyHostToDevice, s));
     if (nnz) {
         SW_TRY(hipMalloc((void **)&k0, nnz * 4));
@@ -760,29 +927,33 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         SW_TRY(hipMalloc((void **)&i0, nnz * 4));
         SW_TRY(hipMalloc((void **)&i1, nnz * 4));
         hipLaunchKernelGGL(k_sweep_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_rp, d_col_src,
-                           p.d_panel_row, P, n, nbuckets, shift, k0, i0);
+                           d_srow, S, n, nbuckets, shift, k0, i0);
         SW_TRY(hipGetLastError());
-        SW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, i0, i1, (int)nnz, 0, end_bit, s));
+        // 64-bit item count: a slice may hold more than 2^31 non-zeros (up to the 32-bit padded
+        // layout checked above)
+        SW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, i0, i1, (uint64_t)nnz, 0, end_bit, s));
         SW_TRY(hipMalloc(&tmp, tmp_bytes));
-        SW_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k0, k1, i0, i1, (int)nnz, 0, end_bit, s));
+        SW_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k0, k1, i0, i1, (uint64_t)nnz, 0, end_bit, s));
         hipLaunchKernelGGL((k_sweep_scatter<ValueType>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, k1,
-                           i1, nnz, nbuckets, d_rp, n, d_col_src, d_val_src, p.d_panel_row, d_off, d_poff,
+                           i1, nnz, nbuckets, d_rp, n, d_col_src, d_val_src, d_srow, d_off, d_poff,
                            p.d_s_col, p.d_s_row, p.d_s_val);
         SW_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL((k_sweep_pad<ValueType>), dim3((P + 255) / 256), dim3(256), 0, s, P, p.d_panel_row, d_off,
-                       d_poff, p.d_s_col, p.d_s_row, p.d_s_val);
+    hipLaunchKernelGGL((k_sweep_pad<ValueType>), dim3((S + 255) / 256), dim3(256), 0, s, S, d_srow, d_off,
+                       d_poff, p.d_s_col, p.d_s_row, p.d_s_val, det);
     SW_TRY(hipGetLastError());
-    // 12-byte packed entries when every 128-entry chunk spans < 65536 columns
+    // 12-byte packed entries when every 128-entry chunk spans < 65536 columns (deterministic
+    // form: every 32-entry quarter chunk, whose segments are W times sparser than a panel)
     {
-        const uint64_t nchunks = p.ent_pad / kSweepChunk;
+        const uint32_t group = det ? kSweepChunk / 4 : kSweepChunk, gshift = det ? 5 : 7;
+        const uint64_t nchunks = p.ent_pad / group;
         SW_TRY(hipMalloc((void **)&p.d_s_cbase, std::max<uint64_t>(nchunks, 1) * 4));
         uint32_t *d_bad = d_off;  // reuse: d_off is no longer needed once the scatter ran
         SW_TRY(hipStreamSynchronize(s));
         SW_TRY(hipMemsetAsync(d_bad, 0, 4, s));
         if (nchunks)
             hipLaunchKernelGGL(k_sweep_chunk_base, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s,
-                               p.d_s_col, nchunks, p.d_s_cbase, d_bad);
+                               p.d_s_col, nchunks, group, p.d_s_cbase, d_bad);
         SW_TRY(hipGetLastError());
         uint32_t bad = 0;
         SW_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
@@ -791,7 +962,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         const bool want = !(env && env[0] == '0');
         if (!bad && want && p.ent_pad) {
             hipLaunchKernelGGL(k_sweep_pack_rc, dim3((unsigned)((p.ent_pad + 255) / 256)), dim3(256), 0, s, p.d_s_col,
-                               p.d_s_row, p.d_s_cbase, p.ent_pad);
+                               p.d_s_row, p.d_s_cbase, p.ent_pad, gshift);
             SW_TRY(hipGetLastError());
             SW_TRY(hipStreamSynchronize(s));
             SW_TRY(hipFree(p.d_s_row));

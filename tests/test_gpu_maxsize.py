@@ -116,16 +116,22 @@ def test_banded_above_2_31_nonzeros(torch, monkeypatch, banded64, kern, want):
     torch.cuda.empty_cache()
 
 
-def test_sweep_refuses_more_than_2_31_nonzeros(torch, monkeypatch, banded64):
+def test_sweep_above_2_31_nonzeros(torch, monkeypatch, banded64):
+    """the sweep's radix sort takes a 64-bit item count, so a slice past 2^31
+    entries stays on the sweep (kernel 2)."""
     lib, rp, col, val, x, rp64, n = banded64
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
-    with pytest.raises(RuntimeError, match="2\\^31-1"):
-        spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    y, st = _run(torch, lib, rp, col, val, x, n, n)
+    assert st["kernel"] == 2
+    _check_sample(torch, rp64, col, val, x, y, _sample_rows(rp64, n, np.random.default_rng(4)), np.float64)
+    _checksum(torch, rp64, col, val, x, y, n, 16_000_000)
+    del y
+    torch.cuda.empty_cache()
 
 
-def test_powerlaw_above_2_31_nonzeros_falls_back_to_tiles(torch):
-    """A 20M-row power-law slice with 2.2e9 non-zeros: the automatic choice would take the sweep
-    (x of 160 MB, random columns) but the sweep cannot hold it, so the plan is the tiles."""
+def test_powerlaw_above_2_31_nonzeros_stays_on_the_sweep(torch):
+    """A 20M-row power-law slice with 2.2e9 non-zeros: x of 160 MB and random columns, so the
+    automatic choice is the panel sweep (kernel 2), whose build now sorts 2.2e9 entries."""
     lib = spmv_hw.load(np.float64)
     n, z = 20_000_000, 2_200_000_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
@@ -133,7 +139,7 @@ def test_powerlaw_above_2_31_nonzeros_falls_back_to_tiles(torch):
     rp64 = _u32(rp)
     assert int(rp64[-1]) == z
     y, st = _run(torch, lib, rp, col, val, x, n, n)
-    assert st["kernel"] == 0
+    assert st["kernel"] == 2
     _check_sample(torch, rp64, col, val, x, y, _sample_rows(rp64, n, np.random.default_rng(2)), np.float64)
     _checksum(torch, rp64, col, val, x, y, n, 2_000_000)
     del rp, col, val, x, rp64, y

@@ -28,8 +28,8 @@ def torch():
     return t
 
 
-KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "gold", "blocked", "slices", "slices_wide"]
-KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "gold": 1, "blocked": 4,
+KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "blocked", "slices", "slices_wide"]
+KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "sweep_det": 2, "gold": 1, "blocked": 4,
              "slices": 5, "slices_wide": 5}
 
 
@@ -39,13 +39,16 @@ def kernel(request, monkeypatch):
     defaults VF = 1, 32768-column blocks); "tiles_wide" is the
     tile kernel with 32-bit columns (SPMV_TILE_NARROW=0) instead of per-tile offsets and
     "sweep_unpacked" the sweep on 14-byte entries (SPMV_SWEEP_PACKED=0), the layout used when a
-    chunk of a panel spans >= 65536 columns; "slices_wide" the slice kernel with 32-bit columns
+    chunk of a panel spans >= 65536 columns; "sweep_det" the deterministic sweep
+    (SPMV_SWEEP_DETERMINISTIC=1); "slices_wide" the slice kernel with 32-bit columns
     (SPMV_SLICE_NARROW=0)."""
     monkeypatch.setenv("SPMV_HW_KERNEL", request.param.split("_")[0])
     if request.param == "tiles_wide":
         monkeypatch.setenv("SPMV_TILE_NARROW", "0")
     if request.param == "sweep_unpacked":
         monkeypatch.setenv("SPMV_SWEEP_PACKED", "0")
+    if request.param == "sweep_det":  # deterministic sweep: one row segment per wave
+        monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
     if request.param == "slices_wide":
         monkeypatch.setenv("SPMV_SLICE_NARROW", "0")
     return request.param

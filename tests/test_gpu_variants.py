@@ -48,3 +48,78 @@ def test_blocked_ablation_variant_is_refused(monkeypatch):
         plan.set_variant(1)
     plan.set_variant(0)
     plan.destroy()
+
+
+# ---- deterministic sweep: env SPMV_SWEEP_DETERMINISTIC=1 ----
+
+def _det_plan(monkeypatch, lib, rp, col, val, n):
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    monkeypatch.delenv("SPMV_SWEEP_DETERMINISTIC")
+    return plan
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_deterministic_sweep_is_bitwise_reproducible(monkeypatch, dtype):
+    """1M-row power-law matrix (16M nnz): five runs of one plan and a run of a second plan built
+    from the same CSR give the same bits, and y meets the oracle (spmv_gold, csr.cpp:184-194)."""
+    import torch
+    import oracle
+    lib = spmv_hw.load(dtype)
+    n, z = 1_000_000, 16_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = _det_plan(monkeypatch, lib, rp, col, val, n)
+    assert plan.stats()["kernel"] == 2 and plan.stats()["format"] & 2
+    ys = []
+    for _ in range(5):
+        y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+        plan.run(x, y)
+        ys.append(y)
+    plan2 = _det_plan(monkeypatch, lib, rp, col, val, n)
+    y2 = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan2.run(x, y2)
+    torch.cuda.synchronize()
+    ref_bits = ys[0].cpu().numpy().view(np.uint8)
+    for y in ys[1:] + [y2]:
+        assert np.array_equal(y.cpu().numpy().view(np.uint8), ref_bits)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref = oracle.spmv_gold(r, c, h[2], h[3])
+    err = oracle.scaled_error(r, c, h[2], h[3], ref, ys[0].cpu().numpy())
+    assert err <= (1e-12 if dtype == np.float64 else 2e-6), err
+    plan.destroy()
+    plan2.destroy()
+
+
+@pytest.mark.parametrize("shape", ["skewed", "empty_rows", "few_rows"])
+def test_deterministic_sweep_edge_shapes(monkeypatch, shape):
+    """Segments with empty rows, panels with fewer rows than waves, one very long row."""
+    import torch
+    import oracle
+    lib = spmv_hw.load(np.float64)
+    rng = np.random.default_rng(7)
+    n = {"skewed": 60_000, "empty_rows": 80_000, "few_rows": 10}[shape]
+    m = 2_000_000
+    if shape == "skewed":
+        lens = rng.integers(1, 20, n)
+        lens[123] = 300_000
+    elif shape == "empty_rows":
+        lens = rng.integers(0, 30, n) * (rng.random(n) < 0.4)
+    else:
+        lens = rng.integers(1, 5000, n)
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    col = np.concatenate([np.sort(rng.choice(m, int(k), replace=False)) for k in lens]).astype(np.uint32)
+    val = rng.uniform(-1, 1, len(col))
+    x = rng.uniform(0, 1, m)
+    t = lambda a: torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).cuda()
+    plan = _det_plan(monkeypatch, lib, t(rp.astype(np.uint32)), t(col), t(val), m)
+    assert plan.stats()["kernel"] == 2
+    y = torch.full((n,), float("nan"), dtype=torch.float64, device="cuda")
+    plan.run(t(x), y)
+    torch.cuda.synchronize()
+    ref = oracle.spmv_gold(rp.astype(np.uint32), col, val, x)
+    assert oracle.scaled_error(rp.astype(np.uint32), col, val, x, ref, y.cpu().numpy()) <= 1e-12
+    plan.destroy()

@@ -98,6 +98,9 @@ def main():
                 if kern.endswith("L"):  # packed, without the lane-order permutation
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_LANE_ORDER"] = "0"
+                if kern.endswith("D"):  # deterministic sweep (one row segment per wave)
+                    kern = kern[:-1]
+                    os.environ["SPMV_SWEEP_DETERMINISTIC"] = "1"
                 if kern.endswith("F32"):  # sweep with the fp32 (CAS) LDS accumulator for fp32 matrices
                     kern = kern[:-3]
                     os.environ["SPMV_SWEEP_ACC"] = "32"
@@ -120,6 +123,7 @@ def main():
                 os.environ.pop("SPMV_FPGA_BLOCK", None)
                 os.environ.pop("SPMV_SWEEP_ACC", None)
                 os.environ.pop("SPMV_SLICE_ACC", None)
+                os.environ.pop("SPMV_SWEEP_DETERMINISTIC", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
