@@ -29,7 +29,8 @@ cpu_baseline (the oracle's restatement of spmv_gold, 1 thread, on the host of th
 parity (full-size componentwise-scaled error vs that oracle run),
 lds_xtiles (power-law, 1 GPU: the same matrix through kernel 4, the reference's dataflow with a
 block of x in LDS per workgroup -- the technique BASELINE configs 3/5 name -- timed beside the
-headline kernel).
+headline kernel), side_configs (1 GPU: BASELINE config 2, banded 1M x 16 fp64, and config 5, the
+power-law matrix in fp32, each timed the same way with its own roofline and oracle parity).
 """
 from __future__ import annotations
 
@@ -71,6 +72,8 @@ def parse():
                     help="N > 1 weak runs: skip the config-4 strong-scaling companion measurement")
     ap.add_argument("--no-weak-companion", action="store_true",
                     help="N > 1 strong runs: skip the weak-scaling companion measurement")
+    ap.add_argument("--no-side-configs", action="store_true",
+                    help="1 GPU: skip the config-2 (banded fp64) and config-5 (power-law fp32) side lines")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the row-parallel CPU line (the box's CPU share is 16)")
@@ -234,6 +237,59 @@ def lds_xtiles(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
            "device_bytes": st["device_bytes"], "max_rel_diff_vs_value_kernel": diff}
     plan.destroy()
     del y
+    torch.cuda.empty_cache()
+    return res
+
+
+def side_config(args, name, dev, stream):
+    """BASELINE configs 2 and 5 beside the headline (1 GPU): the matrix built by the same
+    generator, the automatically chosen kernel timed like the headline (HIP events over K launches
+    after W warm-ups), and y checked against the oracle's spmv_gold on the full matrix."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    dtype = np.float32 if name == "config5" else np.float64
+    lib = spmv_hw.load(dtype)
+    if name == "config2":
+        n = 1_000_000
+        rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
+        x = spmv_hw.gen_vector(lib, n, seed=3)
+        desc = {"workload": "banded", "rows": n, "cols": n, "nnz_per_row": 16, "nnz": 16 * n, "dtype": "f64"}
+    else:
+        n, z = 10_000_000, 160_000_000
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+        x = spmv_hw.gen_vector(lib, n, seed=6)
+        desc = {"workload": "powerlaw", "rows": n, "cols": n, "nnz": z, "dtype": "f32"}
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n, device=dev.index, stream=stream)
+    st = plan.stats()
+    y = torch.empty(n, dtype=x.dtype, device=dev)
+    for _ in range(args.warmup):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    kernel_ms, _, _ = plan.timing()
+    plan.set_timing(False)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref = oracle.spmv_gold(r, c, h[2], h[3])
+    err = oracle.scaled_error(r, c, h[2], h[3], ref, y.cpu().numpy())
+    tol = 1e-6 if dtype == np.float64 else 1e-4
+    alg = st["algorithmic_bytes"]
+    names = {0: "k_spmv_tiles", 2: "k_spmv_sweep_packed" if st["format"] & 2 else "k_spmv_sweep", 5: "k_spmv_slices"}
+    res = {"config": desc, "ms_per_step": round(wall_ms, 5), "kernel_ms": round(kernel_ms, 5),
+           "gflops": round(2.0 * st["nr_nzeros"] / (wall_ms * 1e-3) / 1e9, 3),
+           "effective_GBps": round(alg / (wall_ms * 1e-3) / 1e9, 2),
+           "roofline": {"bound": "hbm", "kernel": names.get(st["kernel"], str(st["kernel"])),
+                        "achieved": round(alg / (kernel_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                        "frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                        "alg_bytes_per_launch": alg},
+           "parity": {"max_scaled_err": err, "tol": tol, "pass": bool(err <= tol)}}
+    plan.destroy()
+    del rp, col, val, x, y
     torch.cuda.empty_cache()
     return res
 
@@ -520,6 +576,12 @@ def main():
     parity = None
     if keep_csr:
         cpu, parity = cpu_baseline(lib, rp, col, val, x, y, args.cpu_reps, args.cpu_threads)
+        del rp, col, val
+        torch.cuda.empty_cache()
+
+    side = None
+    if world == 1 and args.workload == "powerlaw" and args.dtype == "f64" and not args.no_side_configs:
+        side = {name: side_config(args, name, dev, stream) for name in ("config2", "config5")}
 
     if rank == 0:
         out = {
@@ -551,6 +613,7 @@ def main():
             "strong_companion": strong,
             "weak_companion": weak,
             "lds_xtiles": xtiles,
+            "side_configs": side,
             "host_copy": host,
             "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
             "setup_s": round(setup_s, 2),

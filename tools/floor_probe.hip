@@ -23,8 +23,10 @@
 // One JSON line per test: ms (mean of 10 launches after 2 warm-ups), G requests/s.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <vector>
 
 #define CHECK(x)                                                             \
     do {                                                                     \
@@ -240,5 +242,49 @@ int main()
     SWEEPS("sweep_split_roles_l2x", 3, true, true)
 #undef SWEEP
 #undef SWEEPS
+    // Where do the stream and the gathers collide? Half of the CUs (CU mask) stream half of the
+    // entries while the other half gathers half of the x lines, each alone and then at the same
+    // time on two streams. Concurrent ~ max(alone): the collision is inside a CU (in-order vector
+    // memory pipe), and CUs that only pull entries into L2 could feed the sweeping ones.
+    // Concurrent ~ sum: the collision is chip-level (L2 channels / fabric).
+    {
+        hipDeviceProp_t prop;
+        CHECK(hipGetDeviceProperties(&prop, 0));
+        const int cus = prop.multiProcessorCount;
+        std::vector<uint32_t> ma((cus + 31) / 32, 0), mb((cus + 31) / 32, 0);
+        for (int c = 0; c < cus; ++c)
+            ((c & 1) ? mb : ma)[c / 32] |= 1u << (c % 32);
+        hipStream_t sa, sb;
+        CHECK(hipExtStreamCreateWithCUMask(&sa, (uint32_t)ma.size(), ma.data()));
+        CHECK(hipExtStreamCreateWithCUMask(&sb, (uint32_t)mb.size(), mb.data()));
+        const uint32_t half = panels / 2;
+        auto launch_s = [&] { hipLaunchKernelGGL((k_sweep<2, false>), dim3(half), dim3(kT), lds, sa, rc, val, x, m, chunks, sink); };
+        auto launch_g = [&] { hipLaunchKernelGGL((k_sweep<1, false>), dim3(half), dim3(kT), lds, sb, rc, val, x, m, chunks, sink); };
+        CHECK(hipFuncSetAttribute((const void *)k_sweep<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        CHECK(hipFuncSetAttribute((const void *)k_sweep<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        auto wall = [&](const char *name, auto go, double req, double bytes) -> int {
+            for (int w = 0; w < 2; ++w)
+                go();
+            CHECK(hipDeviceSynchronize());
+            const int reps = 10;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int r = 0; r < reps; ++r)
+                go();
+            CHECK(hipDeviceSynchronize());
+            const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / reps;
+            std::printf("{\"test\": \"%s\", \"ms\": %.4f, \"Greq_per_s\": %.2f, \"GBps\": %.1f, \"requests\": %.0f, "
+                        "\"bytes\": %.0f, \"cus_each\": %d}\n",
+                        name, sec * 1e3, req / sec / 1e9, bytes / sec / 1e9, req, bytes, cus / 2);
+            std::fflush(stdout);
+            return 0;
+        };
+        const double hreq = greq / 2, hbytes = sbytes / 2;
+        if (wall("halfcus_stream_alone", [&] { launch_s(); }, 0.0, hbytes))
+            return 1;
+        if (wall("halfcus_gather_alone", [&] { launch_g(); }, hreq, 0.0))
+            return 1;
+        if (wall("halfcus_stream_and_gather_concurrent", [&] { launch_s(); launch_g(); }, hreq, hbytes))
+            return 1;
+    }
     return 0;
 }
