@@ -82,7 +82,10 @@ constexpr uint32_t kT = 1024;       // threads per workgroup (16 waves), as the 
 constexpr uint32_t kChunk = 128;    // entries per chunk (one wave: 2 per lane)
 constexpr uint32_t kRows = 20447;   // fp64 y slots in 160 KiB of LDS
 
-template <int MODE, bool L2X>
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+template <int MODE, bool L2X, int AUX = -1>
 __device__ __forceinline__ void k_sweep_body(const uint32_t *__restrict__ rc, const double *__restrict__ val,
                                              const double *__restrict__ x, uint32_t m, uint32_t chunks_in,
                                              double *__restrict__ sink, uint32_t wg, uint32_t span_panels)
@@ -106,7 +109,17 @@ __device__ __forceinline__ void k_sweep_body(const uint32_t *__restrict__ rc, co
         for (int q = 0; q < 2; ++q) {
             uint32_t c = c0 + q * (kT / 64) + wave;
             c = c < chunks ? c : chunks - 1;
-            if constexpr (MODE & 2) {
+            if constexpr ((MODE & 2) && AUX >= 0) {
+                // buffer loads with explicit cache-policy bits (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+                const uint32_t eo = c * kChunk + 2 * lane;
+                const auto rrc = __builtin_amdgcn_make_buffer_rsrc((void *)(rc + pbase), (short)0, 0x7FFFFFFF, 0x00020000);
+                const auto rvl = __builtin_amdgcn_make_buffer_rsrc((void *)(val + pbase), (short)0, 0x7FFFFFFF, 0x00020000);
+                const u32x2v ww = __builtin_amdgcn_raw_buffer_load_b64(rrc, eo * 4, 0, AUX);
+                const u32x4v vv = __builtin_amdgcn_raw_buffer_load_b128(rvl, eo * 8, 0, AUX);
+                w[q] = make_uint2(ww.x, ww.y);
+                v[q][0] = __builtin_bit_cast(double, ((uint64_t)vv.y << 32) | vv.x);
+                v[q][1] = __builtin_bit_cast(double, ((uint64_t)vv.w << 32) | vv.z);
+            } else if constexpr (MODE & 2) {
                 const uint64_t e = pbase + (uint64_t)c * kChunk + 2 * lane;
                 const u32x2 ww = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(rc + e));
                 const f64x2 vv = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(val + e));
@@ -154,7 +167,7 @@ __device__ __forceinline__ void k_sweep_body(const uint32_t *__restrict__ rc, co
 // MODE bit 0: x gathers, bit 1: entry stream, bit 2: LDS adds; L2X: gathers folded into 2 MiB.
 // SPLIT: workgroups split the roles -- even workgroups only stream, odd ones only gather, each
 // over two panels' worth of chunks (same totals as MODE 3 on every workgroup)
-template <int MODE, bool L2X, bool SPLIT = false>
+template <int MODE, bool L2X, bool SPLIT = false, int AUX = -1>
 __global__ __launch_bounds__(kT) void k_sweep(const uint32_t *__restrict__ rc, const double *__restrict__ val,
                                               const double *__restrict__ x, uint32_t m, uint32_t chunks_in,
                                               double *__restrict__ sink)
@@ -165,7 +178,7 @@ __global__ __launch_bounds__(kT) void k_sweep(const uint32_t *__restrict__ rc, c
             return k_sweep_body<1, L2X>(rc, val, x, m, chunks_in, sink, blockIdx.x - 1, 2);
         return k_sweep_body<2, L2X>(rc, val, x, m, chunks_in, sink, blockIdx.x, 2);
     }
-    return k_sweep_body<MODE, L2X>(rc, val, x, m, chunks_in, sink, blockIdx.x, 1);
+    return k_sweep_body<MODE, L2X, AUX>(rc, val, x, m, chunks_in, sink, blockIdx.x, 1);
 }
 int main()
 {
@@ -238,6 +251,23 @@ int main()
     SWEEP("sweep_full", 7, false)
     SWEEP("sweep_full_l2x", 7, true)
     SWEEP("sweep_lds_only", 4, false)
+#define SWEEPA(NAME, MODE, AUX)                                                                                      \
+    CHECK(hipFuncSetAttribute((const void *)k_sweep<MODE, false, false, AUX>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+    if (timed(NAME, [&] { hipLaunchKernelGGL((k_sweep<MODE, false, false, AUX>), dim3(panels), dim3(kT), lds, 0, rc, val, x, m, chunks, sink); }, \
+              (MODE & 1) ? greq : 0.0, (MODE & 2) ? sbytes : 0.0))                                                  \
+        return 1;
+    // the entry stream with other cache-policy bits (buffer loads; 1 = sc0, 2 = nt, 16 = sc1)
+    SWEEPA("stream_buf_aux0", 2, 0)
+    SWEEPA("stream_buf_aux2_nt", 2, 2)
+    SWEEPA("stream_buf_aux3_sc0nt", 2, 3)
+    SWEEPA("stream_buf_aux18_sc1nt", 2, 18)
+    SWEEPA("stream_buf_aux19_sc0sc1nt", 2, 19)
+    SWEEPA("both_buf_aux2_nt", 3, 2)
+    SWEEPA("both_buf_aux3_sc0nt", 3, 3)
+    SWEEPA("both_buf_aux18_sc1nt", 3, 18)
+    SWEEPA("both_buf_aux19_sc0sc1nt", 3, 19)
+    SWEEPA("both_buf_aux17_sc0sc1", 3, 17)
+#undef SWEEPA
     SWEEPS("sweep_split_roles", 3, false, true)
     SWEEPS("sweep_split_roles_l2x", 3, true, true)
 #undef SWEEP

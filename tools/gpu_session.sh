@@ -45,7 +45,7 @@ for s in $STEPS; do
            run pmc_$tagc 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$tagc" -o run -- python tools/ab_variants.py --workload powerlaw --variants sweep:3,sweep:11 --rounds 1 --reps 3
          done ;;
     pmcw) for wl in powerlaw banded; do for dt in f64 f32; do for c in FETCH_SIZE WRITE_SIZE TCC_HIT_sum TCC_MISS_sum; do
-           run pmc_${wl}_${dt}_$c 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_${dt}_$c" -o run -- python bench.py --workload $wl --dtype $dt --no-cpu --no-xtiles --steps 5 --warmup 1
+           run pmc_${wl}_${dt}_$c 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_${dt}_$c" -o run -- python bench.py --workload $wl --dtype $dt --no-cpu --no-xtiles --no-side-configs --steps 5 --warmup 1
          done; done; done
          python tools/pmc_traffic.py "$OUT" --out "$OUT/traffic.json" > /dev/null ;;
     pmcx) i=0; for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM" \
