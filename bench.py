@@ -72,6 +72,8 @@ def parse():
                     help="N > 1 weak runs: skip the config-4 strong-scaling companion measurement")
     ap.add_argument("--no-weak-companion", action="store_true",
                     help="N > 1 strong runs: skip the weak-scaling companion measurement")
+    ap.add_argument("--no-native-exchange", action="store_true",
+                    help="N > 1: skip the library's own RCCL exchange (spmv_mgpu_create_rank)")
     ap.add_argument("--no-side-configs", action="store_true",
                     help="1 GPU: skip the config-2 (banded fp64) and config-5 (power-law fp32) side lines")
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -291,6 +293,69 @@ def side_config(args, name, dev, stream):
     plan.destroy()
     del rp, col, val, x, y
     torch.cuda.empty_cache()
+    return res
+
+
+def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
+    """The y exchange through the library's own RCCL path (Part 4 of the C-ABI,
+    spmv_mgpu_create_rank): rank 0's RCCL id is shared over torch.distributed, every rank joins
+    with its plan, and spmv_mgpu_run times the SpMV plus each exchange form with HIP events
+    (compute / exchange, max over ranks). rank 0's gathered y is checked against a gather of the
+    same slices through torch.distributed."""
+    ok = torch.tensor([1.0], device=dev)
+    uid = b"\0" * 128
+    try:
+        uid = spmv_hw.mgpu_unique_id(lib)  # every rank: RCCL loads here
+    except Exception:
+        ok.fill_(0.0)
+    t = spmv_dist._staged(torch.tensor(list(uid), dtype=torch.uint8, device=dev))
+    dist.broadcast(t, src=0)
+    uid = bytes(t.cpu().tolist())
+    okt = spmv_dist._staged(ok)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    if float(okt.item()) < 1.0:
+        return {"error": "RCCL could not be loaded on every rank"}
+    bounds = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint32)
+    mg, err = None, None
+    try:
+        mg = spmv_hw.MultiGpu.rank(lib, rank, world, uid, dev.index, bounds, ncols, plan)
+    except Exception as e:  # the clique is formed; agree before any collective
+        err = str(e)[:300]
+    ok.fill_(0.0 if mg is None else 1.0)
+    okt = spmv_dist._staged(ok)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    if float(okt.item()) < 1.0:
+        if mg is not None:
+            mg.destroy()
+        return {"error": err or "spmv_mgpu_create_rank failed on another rank"}
+    res = {"api": "spmv_mgpu_create_rank + spmv_mgpu_run (library RCCL clique, one rank per GPU)"}
+    mg.set_x_device(x)
+    for name, mode in (("gather", spmv_hw.MGPU_GATHER), ("reduce", spmv_hw.MGPU_REDUCE),
+                       ("allgather", spmv_hw.MGPU_ALLGATHER)):
+        if mode == spmv_hw.MGPU_ALLGATHER:
+            mg.set_x_device(x)
+        for _ in range(2):
+            mg.run(mode)
+        cs, es = [], []
+        for _ in range(reps):
+            if mode == spmv_hw.MGPU_ALLGATHER:
+                mg.set_x_device(x)  # every run computes A x, not A^k x
+            mg.run(mode)
+            c, e = mg.timing()
+            cs.append(c)
+            es.append(e)
+        res[f"{name}_compute_ms"] = round(spmv_dist.max_over_ranks(float(np.median(cs)), dev), 5)
+        res[f"{name}_exchange_ms"] = round(spmv_dist.max_over_ranks(float(np.median(es)), dev), 5)
+        if mode == spmv_hw.MGPU_GATHER:
+            y_loc = torch.empty(int(counts[rank]), dtype=x.dtype, device=dev)
+            plan.run(x, y_loc, torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            y_t = spmv_dist.exchange_gather(y_loc, counts)
+            if rank == 0:
+                y_n = torch.from_numpy(mg.y(spmv_hw.MGPU_GATHER)).to(y_t.device)
+                res["gather_max_rel_diff_vs_torch"] = float(
+                    ((y_n.double() - y_t.double()).abs().max() / y_t.double().abs().max().clamp_min(1e-300)).item())
+    mg.destroy()
     return res
 
 
@@ -563,6 +628,11 @@ def main():
         res["e2e_gflops_with_reduce"] = round(2.0 * nnz_all / ((ms + res["reduce_ms"]) * 1e-3) / 1e9, 2)
         res["e2e_gflops_with_allgather"] = round(2.0 * nnz_all / ((ms + res["allgather_ms"]) * 1e-3) / 1e9, 2)
         res["backend"] = dist.get_backend()
+        if not args.no_native_exchange:
+            try:
+                res["native"] = native_exchange(lib, plan, x, st["nr_cols"], counts, world, rank, dev)
+            except Exception as e:  # reported, never fatal to the bench line
+                res["native"] = {"error": str(e)[:300]}
         exchange = res
 
     strong = None

@@ -165,9 +165,22 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange);
 int spmv_mgpu_get_y(spmv_mgpu *mg, ValueType *h_y, int exchange);
 /* last run: kernels (max over devices) and exchange time, ms (HIP events on each device) */
 int spmv_mgpu_get_timing(const spmv_mgpu *mg, double *compute_ms, double *exchange_ms);
-/* row slice and device of rank d */
-int spmv_mgpu_slice(const spmv_mgpu *mg, int d, IndexType *row_begin, IndexType *row_end, int *device);
+/* row slice and device of rank r (device -1 when rank r lives in another process) */
+int spmv_mgpu_slice(const spmv_mgpu *mg, int r, IndexType *row_begin, IndexType *row_end, int *device);
 void spmv_mgpu_destroy(spmv_mgpu *mg);
+/* One process per GPU (e.g. one torch.distributed rank per GPU): rank 0 makes a 128-byte RCCL id
+ * with spmv_mgpu_unique_id, the caller shares it, and every rank joins with its own plan for rows
+ * [bounds[rank], bounds[rank+1]) (bounds[0..nranks], e.g. spmv_partition_rows) on `device`; the
+ * handle borrows the plan. set_x / run / get_y / get_timing then work as above, collectively:
+ * every rank calls them; set_x reads x on rank 0 only, get_y of a gather / reduce answers on rank 0
+ * only. spmv_mgpu_set_x_device takes rank 0's x already on its device. */
+int spmv_mgpu_unique_id(unsigned char *id128);
+int spmv_mgpu_create_rank(spmv_mgpu **mg, int rank, int nranks, const unsigned char *id128, int device,
+                          const IndexType *bounds, IndexType nr_cols, const spmv_plan *plan);
+int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x);
+/* device address of this process's y (rank 0's y for a gather / reduce; the local x = y after
+ * an all-gather), for callers that keep y on the GPU */
+int spmv_mgpu_y_device(spmv_mgpu *mg, int exchange, ValueType **d_y);
 
 /* ---------------- synthetic inputs (bench/test infrastructure) ---------------- */
 /* Banded: n x n, `width` non-zeros per row, columns [clamp(i - width/2, 0, n - width), +width),

@@ -14,6 +14,11 @@
 //   SPMV_MGPU_ALLGATHER every device broadcasts its slice into every device's next x (grouped
 //                       ncclBroadcast = all-gather with unequal counts); the next run computes
 //                       A * y (iterative solvers)
+// Two ways to form the communicator: one process driving every GPU (spmv_mgpu_create,
+// ncclCommInitAll), or one process per GPU (spmv_mgpu_create_rank, ncclCommInitRank with an id
+// made by spmv_mgpu_unique_id on rank 0 and shared by the caller), which is how bench.py's ranks
+// exchange y natively. The exchange code is the same: it loops over the devices this process
+// drives, each with its rank in the clique.
 // RCCL is loaded at run time (dlopen), so the library itself does not depend on it; a process
 // that already loaded RCCL (e.g. PyTorch's) shares that copy.
 #include <dlfcn.h>
@@ -33,6 +38,8 @@ namespace {
 struct Rccl {
     void *h = nullptr;
     decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
     decltype(&ncclCommDestroy) CommDestroy = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
     decltype(&ncclGroupStart) GroupStart = nullptr;
@@ -65,6 +72,8 @@ const Rccl *rccl()
         return nullptr;
 #define SYM(f) r.f = reinterpret_cast<decltype(r.f)>(dlsym(r.h, "nccl" #f))
     SYM(CommInitAll);
+    SYM(CommInitRank);
+    SYM(GetUniqueId);
     SYM(CommDestroy);
     SYM(GetErrorString);
     SYM(GroupStart);
@@ -74,7 +83,7 @@ const Rccl *rccl()
     SYM(Send);
     SYM(Recv);
 #undef SYM
-    if (!r.CommInitAll || !r.CommDestroy || !r.GetErrorString || !r.GroupStart || !r.GroupEnd || !r.Broadcast ||
+    if (!r.CommInitAll || !r.CommInitRank || !r.GetUniqueId || !r.CommDestroy || !r.GetErrorString || !r.GroupStart || !r.GroupEnd || !r.Broadcast ||
         !r.Reduce || !r.Send || !r.Recv) {
         r.h = nullptr;
         return nullptr;
@@ -88,30 +97,47 @@ constexpr ncclDataType_t kNcclValue = sizeof(ValueType) == 8 ? ncclFloat64 : ncc
 
 struct spmv_mgpu {
     const Rccl *nc = nullptr;
-    int ndev = 0;
+    int nloc = 0;                       // devices driven by this process
+    int nranks = 0;                     // ranks of the clique (= slices)
     IndexType nr_rows = 0, nr_cols = 0;
-    std::vector<int> dev;
-    std::vector<IndexType> bounds;      // row slice of device d: [bounds[d], bounds[d+1])
-    std::vector<spmv_plan *> plan;
+    bool owns_plans = true;
+    std::vector<int> dev, rank;         // per local device: HIP device and rank
+    std::vector<IndexType> bounds;      // row slice of rank r: [bounds[r], bounds[r+1])
+    std::vector<const spmv_plan *> plan;
     std::vector<ncclComm_t> comm;
     std::vector<hipStream_t> stream;
     std::vector<ValueType *> x, xnext;  // full-length x on every device; next x (all-gather)
-    std::vector<ValueType *> yslice;    // device d's rows (d > 0; the root computes into y)
+    std::vector<ValueType *> yslice;    // rank > 0: its rows (rank 0 computes into y)
     std::vector<ValueType *> ypart;     // reduce mode: full-length partials, zero outside the slice
-    ValueType *y = nullptr;             // root's full y
+    std::vector<ValueType *> y;         // rank 0 only: the full y
     std::vector<hipEvent_t> ev;         // per device: start, kernels done, exchange done
     double compute_ms = 0, exchange_ms = 0;
 
+    void init(int n)
+    {
+        nloc = n;
+        dev.assign(n, 0);
+        rank.assign(n, 0);
+        plan.assign(n, nullptr);
+        comm.assign(n, nullptr);
+        stream.assign(n, nullptr);
+        x.assign(n, nullptr);
+        xnext.assign(n, nullptr);
+        yslice.assign(n, nullptr);
+        ypart.assign(n, nullptr);
+        y.assign(n, nullptr);
+        ev.assign(3 * n, nullptr);
+    }
     ~spmv_mgpu()
     {
-        for (int d = 0; d < ndev; ++d) {
+        for (int d = 0; d < nloc; ++d) {
             (void)hipSetDevice(dev[d]);
-            if (d < (int)plan.size() && plan[d])
-                spmv_plan_destroy(plan[d]);
-            for (void *p : {(void *)x[d], (void *)xnext[d], (void *)yslice[d], (void *)ypart[d]})
+            if (owns_plans && plan[d])
+                spmv_plan_destroy(const_cast<spmv_plan *>(plan[d]));
+            for (void *p : {(void *)x[d], (void *)xnext[d], (void *)yslice[d], (void *)ypart[d], (void *)y[d]})
                 if (p)
                     (void)hipFree(p);
-            if (d < (int)comm.size() && comm[d] && nc)
+            if (comm[d] && nc)
                 nc->CommDestroy(comm[d]);
             if (stream[d])
                 (void)hipStreamDestroy(stream[d]);
@@ -119,12 +145,32 @@ struct spmv_mgpu {
                 if (ev[3 * d + k])
                     (void)hipEventDestroy(ev[3 * d + k]);
         }
-        if (y) {
-            (void)hipSetDevice(dev[0]);
-            (void)hipFree(y);
-        }
     }
-    IndexType rows(int d) const { return bounds[d + 1] - bounds[d]; }
+    IndexType rows_of(int r) const { return bounds[r + 1] - bounds[r]; }
+    IndexType rows(int d) const { return rows_of(rank[d]); }
+    // buffers every local device needs (stream, events, x, its y slice or the root's y)
+    int alloc_device(int d)
+    {
+        SPMV_TRY(hipSetDevice(dev[d]));
+        SPMV_TRY(hipStreamCreateWithFlags(&stream[d], hipStreamNonBlocking));
+        for (int k = 0; k < 3; ++k)
+            SPMV_TRY(hipEventCreate(&ev[3 * d + k]));
+        const size_t xb = std::max<size_t>(nr_cols, 1) * sizeof(ValueType);
+        SPMV_TRY(hipMalloc((void **)&x[d], xb));
+        SPMV_TRY(hipMemset(x[d], 0, xb));
+        if (rank[d] == 0)
+            SPMV_TRY(hipMalloc((void **)&y[d], std::max<size_t>(nr_rows, 1) * sizeof(ValueType)));
+        else
+            SPMV_TRY(hipMalloc((void **)&yslice[d], std::max<size_t>(rows(d), 1) * sizeof(ValueType)));
+        return 0;
+    }
+    int root_local() const  // local index of rank 0, or -1
+    {
+        for (int d = 0; d < nloc; ++d)
+            if (rank[d] == 0)
+                return d;
+        return -1;
+    }
 };
 
 #define MG_NCCL(expr)                                                                          \
@@ -167,37 +213,23 @@ int spmv_mgpu_create(spmv_mgpu **out, int ndev, const int *devices, const csr_ma
     }
     std::unique_ptr<spmv_mgpu> mg(new spmv_mgpu());
     mg->nc = nc;
-    mg->ndev = ndev;
-    mg->dev = dl;
+    mg->init(ndev);
+    mg->nranks = ndev;
     mg->nr_rows = m->nr_rows;
     mg->nr_cols = m->nr_cols;
-    mg->plan.assign(ndev, nullptr);
-    mg->stream.assign(ndev, nullptr);
-    mg->x.assign(ndev, nullptr);
-    mg->xnext.assign(ndev, nullptr);
-    mg->yslice.assign(ndev, nullptr);
-    mg->ypart.assign(ndev, nullptr);
-    mg->ev.assign(3 * ndev, nullptr);
     mg->bounds.assign(ndev + 1, 0);
     if (spmv_partition_rows(m->row_ptr, m->nr_rows, ndev, mg->bounds.data()))
         return 1;
-    const size_t xb = std::max<size_t>(m->nr_cols, 1) * sizeof(ValueType);
-    const size_t nb = std::max<size_t>(m->nr_rows, 1) * sizeof(ValueType);
     for (int d = 0; d < ndev; ++d) {
-        SPMV_TRY(hipSetDevice(dl[d]));
-        SPMV_TRY(hipStreamCreateWithFlags(&mg->stream[d], hipStreamNonBlocking));
-        for (int k = 0; k < 3; ++k)
-            SPMV_TRY(hipEventCreate(&mg->ev[3 * d + k]));
-        if (spmv_plan_create_host(&mg->plan[d], dl[d], m, mg->bounds[d], mg->bounds[d + 1]))
+        mg->dev[d] = dl[d];
+        mg->rank[d] = d;
+        spmv_plan *pl = nullptr;
+        if (spmv_plan_create_host(&pl, dl[d], m, mg->bounds[d], mg->bounds[d + 1]))
             return 1;
-        SPMV_TRY(hipMalloc((void **)&mg->x[d], xb));
-        SPMV_TRY(hipMemset(mg->x[d], 0, xb));
-        if (d > 0)
-            SPMV_TRY(hipMalloc((void **)&mg->yslice[d], std::max<size_t>(mg->rows(d), 1) * sizeof(ValueType)));
-        else
-            SPMV_TRY(hipMalloc((void **)&mg->y, nb));
+        mg->plan[d] = pl;
+        if (mg->alloc_device(d))
+            return 1;
     }
-    mg->comm.assign(ndev, nullptr);
     {
         ncclResult_t r = nc->CommInitAll(mg->comm.data(), ndev, dl.data());
         if (r != ncclSuccess) {
@@ -210,27 +242,135 @@ int spmv_mgpu_create(spmv_mgpu **out, int ndev, const int *devices, const csr_ma
     return 0;
 }
 
-// x (nr_cols values, host) -> the root device, then one RCCL broadcast to every device
-int spmv_mgpu_set_x(spmv_mgpu *mg, const ValueType *h_x)
+int spmv_mgpu_unique_id(unsigned char *id)
 {
-    if (!mg || !h_x) {
-        set_error("spmv_mgpu_set_x: bad arguments");
+    if (!id) {
+        set_error("spmv_mgpu_unique_id: null argument");
         return 1;
     }
-    SPMV_TRY(hipSetDevice(mg->dev[0]));
-    if (mg->nr_cols && upload_staged(mg->x[0], h_x, size_t(mg->nr_cols) * sizeof(ValueType), mg->stream[0]))
+    const Rccl *nc = rccl();
+    if (!nc) {
+        set_error("spmv_mgpu_unique_id: RCCL (librccl.so.1) could not be loaded");
         return 1;
-    if (mg->ndev == 1 || mg->nr_cols == 0)
+    }
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId u;
+    const ncclResult_t r = nc->GetUniqueId(&u);
+    if (r != ncclSuccess) {
+        set_error(std::string("spmv_mgpu_unique_id: ") + nc->GetErrorString(r));
+        return 1;
+    }
+    std::memcpy(id, &u, sizeof(u));
+    return 0;
+}
+
+int spmv_mgpu_create_rank(spmv_mgpu **out, int rank, int nranks, const unsigned char *id, int device,
+                          const IndexType *bounds, IndexType nr_cols, const spmv_plan *plan)
+{
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || !id || !bounds || !plan) {
+        set_error("spmv_mgpu_create_rank: bad arguments");
+        return 1;
+    }
+    *out = nullptr;
+    for (int r = 0; r < nranks; ++r)
+        if (bounds[r + 1] < bounds[r]) {
+            set_error("spmv_mgpu_create_rank: bounds must be non-decreasing");
+            return 1;
+        }
+    if (plan->nr_rows != bounds[rank + 1] - bounds[rank] || plan->nr_cols != nr_cols || plan->device != device) {
+        set_error("spmv_mgpu_create_rank: the plan is not this rank's slice on `device`");
+        return 1;
+    }
+    const Rccl *nc = rccl();
+    if (!nc) {
+        set_error("spmv_mgpu_create_rank: RCCL (librccl.so.1) could not be loaded");
+        return 1;
+    }
+    std::unique_ptr<spmv_mgpu> mg(new spmv_mgpu());
+    mg->nc = nc;
+    mg->init(1);
+    mg->owns_plans = false;
+    mg->nranks = nranks;
+    mg->bounds.assign(bounds, bounds + nranks + 1);
+    mg->nr_rows = bounds[nranks];
+    mg->nr_cols = nr_cols;
+    mg->dev[0] = device;
+    mg->rank[0] = rank;
+    mg->plan[0] = plan;
+    // join the clique first: a rank that failed before ncclCommInitRank would leave the others
+    // waiting in it; failures after it are reported to the caller, who agrees with the other
+    // ranks before the first collective
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    SPMV_TRY(hipSetDevice(device));
+    const ncclResult_t r = nc->CommInitRank(&mg->comm[0], nranks, u, rank);
+    if (r != ncclSuccess) {
+        mg->comm[0] = nullptr;
+        set_error(std::string("spmv_mgpu_create_rank: ncclCommInitRank: ") + nc->GetErrorString(r));
+        return 1;
+    }
+    if (mg->alloc_device(0))
+        return 1;
+    *out = mg.release();
+    return 0;
+}
+
+// RCCL broadcast of rank 0's x to every device's x, then wait
+static int broadcast_x(spmv_mgpu *mg)
+{
+    if (mg->nranks == 1 || mg->nr_cols == 0)
         return 0;
     MG_NCCL(mg->nc->GroupStart());
-    for (int d = 0; d < mg->ndev; ++d)
-        MG_NCCL(mg->nc->Broadcast(mg->x[0], mg->x[d], mg->nr_cols, kNcclValue, 0, mg->comm[d], mg->stream[d]));
+    for (int d = 0; d < mg->nloc; ++d)
+        MG_NCCL(mg->nc->Broadcast(mg->x[d], mg->x[d], mg->nr_cols, kNcclValue, 0, mg->comm[d], mg->stream[d]));
     MG_NCCL(mg->nc->GroupEnd());
-    for (int d = 0; d < mg->ndev; ++d) {
+    for (int d = 0; d < mg->nloc; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         SPMV_TRY(hipStreamSynchronize(mg->stream[d]));
     }
     return 0;
+}
+
+// x (nr_cols values, host) -> rank 0's device, then one RCCL broadcast to every device. In the
+// one-process-per-GPU form every rank calls it (h_x is read on rank 0 only).
+int spmv_mgpu_set_x(spmv_mgpu *mg, const ValueType *h_x)
+{
+    if (!mg) {
+        set_error("spmv_mgpu_set_x: bad arguments");
+        return 1;
+    }
+    const int r0 = mg->root_local();
+    if (r0 >= 0) {
+        if (!h_x) {
+            set_error("spmv_mgpu_set_x: rank 0 needs x");
+            return 1;
+        }
+        SPMV_TRY(hipSetDevice(mg->dev[r0]));
+        if (mg->nr_cols && upload_staged(mg->x[r0], h_x, size_t(mg->nr_cols) * sizeof(ValueType), mg->stream[r0]))
+            return 1;
+    }
+    return broadcast_x(mg);
+}
+
+// the same from a device-resident x on rank 0's device
+int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x)
+{
+    if (!mg) {
+        set_error("spmv_mgpu_set_x_device: bad arguments");
+        return 1;
+    }
+    const int r0 = mg->root_local();
+    if (r0 >= 0) {
+        if (!d_x) {
+            set_error("spmv_mgpu_set_x_device: rank 0 needs x");
+            return 1;
+        }
+        SPMV_TRY(hipSetDevice(mg->dev[r0]));
+        if (mg->nr_cols)
+            SPMV_TRY(hipMemcpyAsync(mg->x[r0], d_x, size_t(mg->nr_cols) * sizeof(ValueType), hipMemcpyDeviceToDevice,
+                                    mg->stream[r0]));
+    }
+    return broadcast_x(mg);
 }
 
 int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
@@ -243,64 +383,66 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
         set_error("spmv_mgpu_run: the all-gather exchange makes y the next x (needs a square matrix)");
         return 1;
     }
-    const int nd = mg->ndev;
+    const int nl = mg->nloc, nr = mg->nranks;
     const size_t nb = size_t(mg->nr_rows) * sizeof(ValueType);
     // buffers of the exchange form, allocated on first use
-    for (int d = 0; d < nd; ++d) {
+    for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
-        if (exchange == 1 && nd > 1 && !mg->ypart[d])
+        if (exchange == 1 && nr > 1 && !mg->ypart[d])
             SPMV_TRY(hipMalloc((void **)&mg->ypart[d], std::max<size_t>(nb, sizeof(ValueType))));
         if (exchange == 2 && !mg->xnext[d])
             SPMV_TRY(hipMalloc((void **)&mg->xnext[d], std::max<size_t>(nb, sizeof(ValueType))));
     }
     // where device d's kernels write its rows
     auto dst = [&](int d) -> ValueType * {
+        const IndexType b = mg->bounds[mg->rank[d]];
         if (exchange == 2)
-            return mg->xnext[d] + mg->bounds[d];
-        if (exchange == 1 && nd > 1)
-            return mg->ypart[d] + mg->bounds[d];
-        return d == 0 ? mg->y + mg->bounds[0] : mg->yslice[d];
+            return mg->xnext[d] + b;
+        if (exchange == 1 && nr > 1)
+            return mg->ypart[d] + b;
+        return mg->rank[d] == 0 ? mg->y[d] + b : mg->yslice[d];
     };
-    for (int d = 0; d < nd; ++d) {
+    for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         hipStream_t s = mg->stream[d];
         SPMV_TRY(hipEventRecord(mg->ev[3 * d], s));
-        if (exchange == 1 && nd > 1)  // full-length partial: zero outside the slice
+        if (exchange == 1 && nr > 1)  // full-length partial: zero outside the slice
             SPMV_TRY(hipMemsetAsync(mg->ypart[d], 0, nb, s));
         if (mg->rows(d) && spmv_plan_run(mg->plan[d], mg->x[d], dst(d), s))
             return 1;
         SPMV_TRY(hipEventRecord(mg->ev[3 * d + 1], s));
     }
-    if (nd > 1 && mg->nr_rows) {
+    if (nr > 1 && mg->nr_rows) {
         MG_NCCL(mg->nc->GroupStart());
-        for (int d = 0; d < nd; ++d) {
+        for (int d = 0; d < nl; ++d) {
             hipStream_t s = mg->stream[d];
+            const int rk = mg->rank[d];
             if (exchange == 0) {
-                if (d == 0) {
-                    for (int p = 1; p < nd; ++p)
-                        if (mg->rows(p))
-                            MG_NCCL(mg->nc->Recv(mg->y + mg->bounds[p], mg->rows(p), kNcclValue, p, mg->comm[0], s));
+                if (rk == 0) {
+                    for (int p = 1; p < nr; ++p)
+                        if (mg->rows_of(p))
+                            MG_NCCL(mg->nc->Recv(mg->y[d] + mg->bounds[p], mg->rows_of(p), kNcclValue, p, mg->comm[d], s));
                 } else if (mg->rows(d)) {
                     MG_NCCL(mg->nc->Send(mg->yslice[d], mg->rows(d), kNcclValue, 0, mg->comm[d], s));
                 }
             } else if (exchange == 1) {
-                MG_NCCL(mg->nc->Reduce(mg->ypart[d], d == 0 ? mg->y : nullptr, mg->nr_rows, kNcclValue, ncclSum, 0,
+                MG_NCCL(mg->nc->Reduce(mg->ypart[d], rk == 0 ? mg->y[d] : nullptr, mg->nr_rows, kNcclValue, ncclSum, 0,
                                        mg->comm[d], s));
             } else {
-                for (int r = 0; r < nd; ++r)  // slice r from its owner into every device's next x
-                    if (mg->rows(r))
+                for (int r = 0; r < nr; ++r)  // slice r from its owner into every device's next x
+                    if (mg->rows_of(r))
                         MG_NCCL(mg->nc->Broadcast(mg->xnext[d] + mg->bounds[r], mg->xnext[d] + mg->bounds[r],
-                                                  mg->rows(r), kNcclValue, r, mg->comm[d], s));
+                                                  mg->rows_of(r), kNcclValue, r, mg->comm[d], s));
             }
         }
         MG_NCCL(mg->nc->GroupEnd());
     }
     double cmax = 0, tmax = 0;
-    for (int d = 0; d < nd; ++d) {
+    for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         SPMV_TRY(hipEventRecord(mg->ev[3 * d + 2], mg->stream[d]));
     }
-    for (int d = 0; d < nd; ++d) {
+    for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         SPMV_TRY(hipEventSynchronize(mg->ev[3 * d + 2]));
         float c = 0, t = 0;
@@ -312,12 +454,12 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
     mg->compute_ms = cmax;
     mg->exchange_ms = std::max(0.0, tmax - cmax);
     if (exchange == 2)
-        for (int d = 0; d < nd; ++d)
+        for (int d = 0; d < nl; ++d)
             std::swap(mg->x[d], mg->xnext[d]);  // y becomes the next x on every device
     return 0;
 }
 
-// y (nr_rows values) to the host: the root's y after a gather / reduce, device 0's x after an
+// y (nr_rows values) to the host: rank 0's y after a gather / reduce, any rank's x after an
 // all-gather (that run's y)
 int spmv_mgpu_get_y(spmv_mgpu *mg, ValueType *h_y, int exchange)
 {
@@ -325,10 +467,32 @@ int spmv_mgpu_get_y(spmv_mgpu *mg, ValueType *h_y, int exchange)
         set_error("spmv_mgpu_get_y: bad arguments");
         return 1;
     }
-    SPMV_TRY(hipSetDevice(mg->dev[0]));
-    const ValueType *src = exchange == 2 ? mg->x[0] : mg->y;
+    const int d = exchange == 2 ? 0 : mg->root_local();
+    if (d < 0) {
+        set_error("spmv_mgpu_get_y: y of a gather / reduce is on rank 0 only");
+        return 1;
+    }
+    SPMV_TRY(hipSetDevice(mg->dev[d]));
+    const ValueType *src = exchange == 2 ? mg->x[d] : mg->y[d];
     if (mg->nr_rows)
         SPMV_TRY(hipMemcpy(h_y, src, size_t(mg->nr_rows) * sizeof(ValueType), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// device address of this process's y: rank 0's full y (gather / reduce), else the local device's
+// x (all-gather: that run's y) -- for callers that keep y on the GPU
+int spmv_mgpu_y_device(spmv_mgpu *mg, int exchange, ValueType **d_y)
+{
+    if (!mg || !d_y || exchange < 0 || exchange > 2) {
+        set_error("spmv_mgpu_y_device: bad arguments");
+        return 1;
+    }
+    const int d = exchange == 2 ? 0 : mg->root_local();
+    if (d < 0) {
+        set_error("spmv_mgpu_y_device: y of a gather / reduce is on rank 0 only");
+        return 1;
+    }
+    *d_y = exchange == 2 ? mg->x[d] : mg->y[d];
     return 0;
 }
 
@@ -345,18 +509,23 @@ int spmv_mgpu_get_timing(const spmv_mgpu *mg, double *compute_ms, double *exchan
     return 0;
 }
 
-int spmv_mgpu_slice(const spmv_mgpu *mg, int d, IndexType *row_begin, IndexType *row_end, int *device)
+// row slice and HIP device of rank r (device -1 when rank r lives in another process)
+int spmv_mgpu_slice(const spmv_mgpu *mg, int r, IndexType *row_begin, IndexType *row_end, int *device)
 {
-    if (!mg || d < 0 || d >= mg->ndev) {
+    if (!mg || r < 0 || r >= mg->nranks) {
         set_error("spmv_mgpu_slice: bad arguments");
         return 1;
     }
     if (row_begin)
-        *row_begin = mg->bounds[d];
+        *row_begin = mg->bounds[r];
     if (row_end)
-        *row_end = mg->bounds[d + 1];
-    if (device)
-        *device = mg->dev[d];
+        *row_end = mg->bounds[r + 1];
+    if (device) {
+        *device = -1;
+        for (int d = 0; d < mg->nloc; ++d)
+            if (mg->rank[d] == r)
+                *device = mg->dev[d];
+    }
     return 0;
 }
 

@@ -103,7 +103,8 @@ EXPORTS = [
     "spmv_gen_banded", "spmv_gen_powerlaw_row_ptr", "spmv_gen_fill", "spmv_gen_vector",
     "spmv_read_csr_header", "spmv_read_csr_matrix", "spmv_read_csr", "spmv_free_csr",
     "spmv_mgpu_create", "spmv_mgpu_set_x", "spmv_mgpu_run", "spmv_mgpu_get_y", "spmv_mgpu_get_timing",
-    "spmv_mgpu_slice", "spmv_mgpu_destroy",
+    "spmv_mgpu_slice", "spmv_mgpu_destroy", "spmv_mgpu_unique_id", "spmv_mgpu_create_rank",
+    "spmv_mgpu_set_x_device", "spmv_mgpu_y_device",
 ]
 
 MGPU_GATHER, MGPU_REDUCE, MGPU_ALLGATHER = 0, 1, 2  # include/csr_hw_wrapper.h SPMV_MGPU_*
@@ -172,6 +173,11 @@ class Lib:
                                                     ctypes.POINTER(ctypes.c_double)]),
             "spmv_mgpu_slice": (ctypes.c_int, [vp, ctypes.c_int, up, up, ctypes.POINTER(ctypes.c_int)]),
             "spmv_mgpu_destroy": (None, [vp]),
+            "spmv_mgpu_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+            "spmv_mgpu_create_rank": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                                     ctypes.c_int, up, IndexType, vp]),
+            "spmv_mgpu_set_x_device": (ctypes.c_int, [vp, vp]),
+            "spmv_mgpu_y_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -364,16 +370,50 @@ class Plan:
             pass
 
 
-class MultiGpu:
-    """Part 4 of the C-ABI (spmv_mgpu_*): one process, `ndev` GPUs, RCCL exchange of y."""
+def mgpu_unique_id(lib: "Lib") -> bytes:
+    """spmv_mgpu_unique_id: the 128-byte RCCL id rank 0 shares with the other ranks."""
+    buf = ctypes.create_string_buffer(128)
+    lib._ok(lib.L.spmv_mgpu_unique_id(buf), "spmv_mgpu_unique_id")
+    return buf.raw
 
-    def __init__(self, lib: Lib, matrix, devices=None, ndev: int = None):
+
+class MultiGpu:
+    """Part 4 of the C-ABI (spmv_mgpu_*): RCCL exchange of y between GPUs -- one process driving
+    `ndev` GPUs (MultiGpu(lib, matrix, ndev=...)), or one process per GPU
+    (MultiGpu.rank(lib, rank, nranks, uid, device, bounds, nr_cols, plan))."""
+
+    def __init__(self, lib: Lib, matrix=None, devices=None, ndev: int = None, _handle=None, _dims=None):
         self.lib = lib
+        if _handle is not None:
+            self.h = _handle
+            self.ndev, self.nr_rows, self.nr_cols = _dims
+            return
         devs = list(devices) if devices is not None else list(range(ndev or 1))
         arr = (ctypes.c_int * len(devs))(*devs)
         h = ctypes.c_void_p()
         lib._ok(lib.L.spmv_mgpu_create(ctypes.byref(h), len(devs), arr, ctypes.byref(matrix)), "spmv_mgpu_create")
         self.h, self.ndev, self.nr_rows, self.nr_cols = h, len(devs), int(matrix.nr_rows), int(matrix.nr_cols)
+
+    @classmethod
+    def rank(cls, lib: Lib, rank: int, nranks: int, uid: bytes, device: int, bounds, nr_cols: int, plan):
+        b = np.ascontiguousarray(bounds, np.uint32)
+        h = ctypes.c_void_p()
+        lib._ok(lib.L.spmv_mgpu_create_rank(ctypes.byref(h), int(rank), int(nranks), uid, int(device),
+                                            b.ctypes.data_as(ctypes.POINTER(IndexType)), int(nr_cols), plan.h),
+                "spmv_mgpu_create_rank")
+        obj = cls(lib, _handle=h, _dims=(1, int(b[-1]), int(nr_cols)))
+        obj._plan = plan  # borrowed by the handle: keep it alive
+        return obj
+
+    def set_x_device(self, x) -> None:
+        """Every rank calls it; x (a device tensor) is read on rank 0 only."""
+        self.lib._ok(self.lib.L.spmv_mgpu_set_x_device(self.h, ctypes.c_void_p(x.data_ptr() if x is not None else 0)),
+                     "spmv_mgpu_set_x_device")
+
+    def y_device_ptr(self, exchange: int = MGPU_GATHER) -> int:
+        p = ctypes.c_void_p()
+        self.lib._ok(self.lib.L.spmv_mgpu_y_device(self.h, int(exchange), ctypes.byref(p)), "spmv_mgpu_y_device")
+        return int(p.value or 0)
 
     def set_x(self, x) -> None:
         x = np.ascontiguousarray(x, self.lib.dtype)

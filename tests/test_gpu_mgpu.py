@@ -92,3 +92,45 @@ def test_mgpu_rejects_bad_devices():
         spmv_hw.MultiGpu(lib, m, devices=[_ndev()])
     with pytest.raises(RuntimeError, match="appears twice"):
         spmv_hw.MultiGpu(lib, m, devices=[0, 0])
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_mgpu_rank_mode_single_rank(dtype):
+    """The one-process-per-GPU form (spmv_mgpu_create_rank: RCCL id from spmv_mgpu_unique_id,
+    ncclCommInitRank, the caller's own plan) as rank 0 of 1: all three exchanges, x from a device
+    tensor, y read back on the host and as a device address. bench.py --gpus N uses the same
+    calls on every rank."""
+    import torch
+    lib = spmv_hw.load(dtype)
+    n, z = 200_000, 3_200_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    uid = spmv_hw.mgpu_unique_id(lib)
+    assert len(uid) == 128
+    mg = spmv_hw.MultiGpu.rank(lib, 0, 1, uid, 0, [0, n], n, plan)
+    assert mg.slice(0) == (0, n, 0)
+    mg.set_x_device(x)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref = oracle.spmv_gold(r, c, h[2], h[3])
+    for ex in (spmv_hw.MGPU_GATHER, spmv_hw.MGPU_REDUCE):
+        mg.run(ex)
+        assert oracle.scaled_error(r, c, h[2], h[3], ref, mg.y(ex)) <= TOL[np.dtype(dtype)]
+        assert mg.y_device_ptr(ex) != 0
+    mg.run(spmv_hw.MGPU_ALLGATHER)
+    y1 = mg.y(spmv_hw.MGPU_ALLGATHER)
+    assert oracle.scaled_error(r, c, h[2], h[3], ref, y1) <= TOL[np.dtype(dtype)]
+    mg.destroy()
+    plan.destroy()
+
+
+def test_mgpu_rank_mode_rejects_a_foreign_plan():
+    lib = spmv_hw.load(np.float64)
+    n = 10_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 160_000, seed=4)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    uid = spmv_hw.mgpu_unique_id(lib)
+    with pytest.raises(RuntimeError, match="not this rank's slice"):
+        spmv_hw.MultiGpu.rank(lib, 0, 1, uid, 0, [0, n - 1], n, plan)
+    plan.destroy()
