@@ -17,9 +17,10 @@ from test_gpu_parity import KERNEL_ID, _bitwise, check, run_device
 pytestmark = pytest.mark.gpu
 
 SEEDS = list(range(48))
-FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "gold", "slices", "slices_wide", "slices_acc32",
-                "fpga", "blocked", "auto", "tune"]
+FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "slices", "slices_wide",
+                "slices_acc32", "fpga", "blocked", "auto", "tune"]
 ENV = {"tiles_wide": {"SPMV_TILE_NARROW": "0"}, "sweep_unpacked": {"SPMV_SWEEP_PACKED": "0"},
+       "sweep_det": {"SPMV_SWEEP_DETERMINISTIC": "1"},
        "slices_wide": {"SPMV_SLICE_NARROW": "0"}, "slices_acc32": {"SPMV_SLICE_ACC": "32"}}
 
 
@@ -109,4 +110,7 @@ def test_fuzz(torch, monkeypatch, seed, kern, dtype):
         _bitwise(y, oracle.spmv_gold(row_ptr, col, val, x))
     elif kern in ("fpga", "blocked"):
         _bitwise(y, oracle.spmv_fpga_order(row_ptr, col, val, x, m, block, vf))
+    elif kern == "sweep_det":  # the deterministic sweep gives the same bits again
+        y2, _ = run_device(torch, lib, row_ptr, col, val, x, m)
+        _bitwise(y2, y)
     check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y, dtype)
