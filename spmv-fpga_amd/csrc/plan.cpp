@@ -826,14 +826,14 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
 
 int spmv_plan_set_variant(spmv_plan *p, int variant)
 {
-    if (!p || variant < 0 || variant > 63) {
+    if (!p || variant < 0 || variant > 127) {
         set_error("spmv_plan_set_variant: bad arguments");
         return 1;
     }
 #ifndef SPMV_ABLATIONS
     // the measurement-only ablations (some give a wrong y by design) exist only in the tools
     // library built with -DSPMV_ABLATIONS (Makefile target `ablations`, tools/ab_variants.py)
-    if ((p->kernel == kKernelSweep && variant >= 54) || (p->kernel == kKernelBlocked && variant == 1)) {
+    if ((p->kernel == kKernelSweep && variant >= 53 && variant <= 63) || (p->kernel == kKernelBlocked && variant == 1)) {
         set_error("spmv_plan_set_variant: measurement-only ablation variant (tools library only)");
         return 1;
     }

@@ -287,7 +287,11 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
             const uint64_t e = wbase + lane2;
             w[q] = lds_<NT>(reinterpret_cast<const u32x2 *>(rc + e));
             cb[q] = cbase[wbase >> 7];
-            loadv<NT, 2>(val, e, v[q]);
+            if constexpr (ABL == 10) {  // ablation: one value per two entries (8 B/entry streamed, not 12)
+                v[q][0] = v[q][1] = lds_<NT>(val + (wbase >> 1) + (lane2 >> 1));
+            } else {
+                loadv<NT, 2>(val, e, v[q]);
+            }
         }
         V xv[Q][2];
 #pragma unroll
@@ -350,6 +354,102 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     }
     if constexpr (ABL == 8 || ABL == 9)
         lds_add(&ylds[R], sink);
+    __syncthreads();
+    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
+}
+
+// Turn-ordered form of k_spmv_sweep_packed: the same plan, layout and gathers, but the LDS adds
+// of a workgroup are ordered. An LDS token `turn` passes from wave to wave: wave w adds the
+// products of its iteration i only when turn == i * W + w, waits for its adds to complete, then
+// hands the token on. Every row therefore receives its products in the fixed order (iteration,
+// wave, lane) that the plan alone defines, so y is bitwise the same on every run -- the
+// fixed-order accumulation of compute_results (spmv.cpp:66-104), in an order of its own -- while
+// each gather instruction still covers 64 consecutive column-sorted entries of the whole panel.
+// The token serialises only the short add phases; a wave that has handed it on issues its next
+// entry loads and gathers at once (PREF: the next iteration's entries are loaded before the
+// wait). SLEEP: s_sleep argument of the polling loop (0 = tight spin).
+template <typename V, int T, int Q, int SLEEP, bool PREF, typename A = double>
+__global__ __launch_bounds__(T) void k_spmv_sweep_turn(
+    const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
+    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
+    const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
+    A *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
+{
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    constexpr uint32_t W = T / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    A *ylds = reinterpret_cast<A *>(smem);
+    __shared__ uint32_t turn;
+    const uint32_t p = unit_panel[blockIdx.x];
+    const uint32_t pieces = panel_unit[p + 1] - panel_unit[p];
+    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
+    const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
+    for (uint32_t i = threadIdx.x; i <= R; i += T)
+        ylds[i] = A(0);
+    if (threadIdx.x == 0)
+        turn = 0;
+    __syncthreads();
+    constexpr uint64_t kGroup = 2ull * T;
+    constexpr uint64_t kStep = Q * kGroup;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane2 = 2u * (threadIdx.x & 63);
+    const uint64_t last_chunk = e1 > e0 ? e1 - 128 : e0;
+    u32x2 w[Q];
+    uint32_t cb[Q];
+    V v[Q][2];
+    bool ok[Q];
+    auto load = [&](uint64_t base, u32x2 (&w_)[Q], uint32_t (&cb_)[Q], V (&v_)[Q][2], bool (&ok_)[Q]) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            uint64_t wbase = base + q * kGroup + 128ull * wave;
+            ok_[q] = wbase < e1;  // wave-uniform; a group past the end re-reads the last chunk
+            wbase = ok_[q] ? wbase : last_chunk;
+            const uint64_t e = wbase + lane2;
+            w_[q] = lds_<true>(reinterpret_cast<const u32x2 *>(rc + e));
+            cb_[q] = cbase[wbase >> 7];
+            loadv<true, 2>(val, e, v_[q]);
+        }
+    };
+    if constexpr (PREF)
+        load(e0, w, cb, v, ok);
+    uint32_t my = wave;  // token value of this wave's current iteration
+    for (uint64_t base = e0; base < e1; base += kStep, my += W) {
+        if constexpr (!PREF)
+            load(base, w, cb, v, ok);
+        V xv[Q][2];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            xv[q][0] = x[cb[q] + (w[q].x & 0xFFFFu)];
+            xv[q][1] = x[cb[q] + (w[q].y & 0xFFFFu)];
+        }
+        uint32_t ri[2 * Q];
+        V vc[Q][2];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            ri[2 * q] = ok[q] ? (w[q].x >> 16) : R;
+            ri[2 * q + 1] = ok[q] ? (w[q].y >> 16) : R;
+            vc[q][0] = v[q][0];
+            vc[q][1] = v[q][1];
+        }
+        if constexpr (PREF)
+            load(base + kStep, w, cb, v, ok);  // next iteration (past the end: the last chunk, unused)
+        A pv[2 * Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            pv[2 * q] = A(vc[q][0]) * A(xv[q][0]);
+            pv[2 * q + 1] = A(vc[q][1]) * A(xv[q][1]);
+        }
+        // wait for the token, add, let the adds complete, hand the token on
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) !=
+               my) {
+            if constexpr (SLEEP > 0)
+                __builtin_amdgcn_s_sleep(SLEEP);
+        }
+        lds_add_n<2 * Q>(ylds, ri, pv);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's adds are done
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_store(&turn, my + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     __syncthreads();
     write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
 }
@@ -662,7 +762,20 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 55: if (p.nr_cols >= 32768) { PKA(9); } else { PK(2, 2); } break;  // no LDS adds, all L2
         case 57: PKA(6); break;  // x gathers with the nt bit
         case 58: PKA(7); break;  // x gathers that bypass L1 (sc1)
+        case 53: PKA(10); break;  // half the value bytes: 8 B/entry streamed instead of 12
 #endif
+#define TURN(Q, SLEEP, PREF)                                                                      \
+    launch_or_warm(warm, k_spmv_sweep_turn<ValueType, T, Q, SLEEP, PREF, A>, grid, block, lds, s, p.d_s_col, \
+                   p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part,   \
+                   p.panel_rmax + 1, d_x, d_y)
+        // 70-75: turn-ordered adds (bitwise reproducible y)
+        case 70: TURN(2, 1, false); break;
+        case 71: TURN(2, 0, false); break;
+        case 72: TURN(2, 1, true); break;
+        case 73: TURN(2, 0, true); break;
+        case 74: TURN(4, 1, true); break;
+        case 75: TURN(4, 0, true); break;
+#undef TURN
         default: PK(2, 2); break;
         }
 #undef PKA

@@ -1,6 +1,6 @@
 """Kernel variants through the product library's C-ABI (spmv_plan_set_variant).
 
-VERDICT r1 item 6: the measurement-only ablations (sweep variants 54-63, blocked variant 1;
+VERDICT r1 item 6: the measurement-only ablations (sweep variants 53-63, blocked variant 1;
 several give a wrong y by design) exist only in the tools library built with -DSPMV_ABLATIONS
 (`make -C spmv-fpga_amd ablations`); the shipped library refuses them with an error code."""
 import numpy as np
@@ -26,7 +26,7 @@ def test_sweep_ablation_variants_are_refused(monkeypatch, dtype):
     assert plan.stats()["kernel"] == 2
     y_ref = torch.empty(x.numel(), dtype=x.dtype, device="cuda")
     plan.run(x, y_ref)
-    for v in range(54, 64):
+    for v in range(53, 64):
         with pytest.raises(RuntimeError, match="measurement-only"):
             plan.set_variant(v)
     # the refusal leaves the plan on its previous (default) variant: same y, bit for bit up to
@@ -122,4 +122,40 @@ def test_deterministic_sweep_edge_shapes(monkeypatch, shape):
     torch.cuda.synchronize()
     ref = oracle.spmv_gold(rp.astype(np.uint32), col, val, x)
     assert oracle.scaled_error(rp.astype(np.uint32), col, val, x, ref, y.cpu().numpy()) <= 1e-12
+    plan.destroy()
+
+
+# ---- turn-ordered sweep: the default layout with LDS adds ordered by a wave-to-wave token ----
+
+@pytest.mark.parametrize("variant", [70, 71, 72, 73, 74, 75])
+@pytest.mark.parametrize("n,z,dtype", [(1_000_000, 16_000_000, np.float64),
+                                       (1_000_000, 16_000_000, np.float32),
+                                       (3_000_000, 48_000_000, np.float64)])
+def test_turn_sweep_is_bitwise_reproducible(monkeypatch, variant, n, z, dtype):
+    """Every turn variant: five runs give the same bits and y meets the oracle. The 1M-row
+    matrix cuts its panels into column pieces (partials + k_sweep_combine), the 3M-row one runs
+    whole panels."""
+    import torch
+    import oracle
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    lib = spmv_hw.load(dtype)
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    assert plan.stats()["kernel"] == 2 and plan.stats()["format"] & 2
+    plan.set_variant(variant)
+    ys = []
+    for _ in range(5):
+        y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+        plan.run(x, y)
+        ys.append(y)
+    torch.cuda.synchronize()
+    ref_bits = ys[0].cpu().numpy().view(np.uint8)
+    for y in ys[1:]:
+        assert np.array_equal(y.cpu().numpy().view(np.uint8), ref_bits)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref = oracle.spmv_gold(r, c, h[2], h[3])
+    err = oracle.scaled_error(r, c, h[2], h[3], ref, ys[0].cpu().numpy())
+    assert err <= (1e-12 if dtype == np.float64 else 2e-6), err
     plan.destroy()

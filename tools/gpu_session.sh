@@ -32,6 +32,7 @@ for s in $STEPS; do
     calib) [ -x tools/hbm_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/hbm_calib.hip -o tools/hbm_calib
            run calib 300 tools/hbm_calib ;;
     strong) run strong 600 python tools/strong_slices.py ${STRONG_ARGS:-} ;;
+    profstrong) run rocprof_strong 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_strong" -o run -- python tools/strong_slices.py ${STRONG_ARGS:---ns 4,8} ;;
     skew) run skew 600 python tools/skew_probe.py ${SKEW_ARGS:-} ;;
     e2e) run reader 600 python tools/bench_reader.py --dir /tmp --threads 1,8,16
          run run_elf_16m 600 ./tests/run_elf/run.elf /tmp/reader_1000000_16000000.mtx --fast-reader ;;
