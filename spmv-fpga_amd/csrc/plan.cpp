@@ -602,7 +602,7 @@ spmv_plan::~spmv_plan()
                       (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
-                      (void *)d_sbase, (void *)d_slice_len, (void *)d_seg_row})
+                      (void *)d_sbase, (void *)d_slice_len})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -626,9 +626,8 @@ uint64_t spmv_plan::device_bytes() const
                (uint64_t(nr_rows) + 1) * 4 + (nchunks + 1) * 4 + nunits * 8 + 4;
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
-               (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / (sweep_det ? kSweepChunk / 4 : kSweepChunk) * 4 : 0) +
-               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * sweep_acc_bytes : 0) + nunits * 4 + (npanels + 1) * 4 +
-               (sweep_det ? 2 * npanels * (uint64_t(sweep_threads) / kWave) * 4 + 4 : 0);  // segment rows + entries
+               (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
+               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * sweep_acc_bytes : 0) + nunits * 4 + (npanels + 1) * 4;
     return nnz_pad * (tile_col_bytes + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
            (tile_col_bytes < 4 ? ntiles * (tile_clustered ? 16 : 4) : 0) +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;
@@ -826,7 +825,7 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
 
 int spmv_plan_set_variant(spmv_plan *p, int variant)
 {
-    if (!p || variant < 0 || variant > 127) {
+    if (!p || variant < 0 || (variant > 63 && variant != kSweepTurn && variant != kSweepTurnOrdered)) {
         set_error("spmv_plan_set_variant: bad arguments");
         return 1;
     }

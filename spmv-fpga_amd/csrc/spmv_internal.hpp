@@ -40,6 +40,8 @@ constexpr int kBlockThreads = 256;                 // 4 waves = 4 tiles per work
 constexpr int kSweepThreads = 1024;                // default panel-sweep workgroup (16 waves, 1/CU)
 constexpr uint64_t kSweepLdsBytes = 160 * 1024;    // LDS of one CU holds the panel's y
 constexpr uint64_t kSweepChunk = 128;              // entries per packed chunk (one wave, 2 per lane)
+constexpr int kSweepTurn = 91;         // sweep variant: ordered LDS adds (deterministic y), the
+constexpr int kSweepTurnOrdered = 94;  // form of SPMV_SWEEP_DETERMINISTIC=1; 94: adds awaited
 
 // plan kernels (spmv_plan_stats.kernel)
 constexpr int kKernelTiles = 0;  // flagged-tile wave kernel, x gathered through the caches
@@ -126,8 +128,7 @@ struct spmv_plan {
     uint32_t *d_s_cbase = nullptr;   // packed form: base column per 128-entry chunk
     bool sweep_packed = false;
     bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)
-    bool sweep_det = false;          // env SPMV_SWEEP_DETERMINISTIC=1: one segment per wave (sweep.hip)
-    uint32_t *d_seg_row = nullptr;   // deterministic form: row ranges of the wave segments [npanels * waves + 1]
+    bool sweep_det = false;          // env SPMV_SWEEP_DETERMINISTIC=1: ordered LDS adds (k_spmv_sweep_turn)
     double locality = -1.0;    // probe result used by the automatic kernel choice
     double tuned_ms[3] = {-1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: measured tiles / sweep / slices ms
 

@@ -83,10 +83,6 @@ __device__ __forceinline__ void lds_add_n(float *y, const uint32_t (&idx)[N], co
     }
 }
 
-// sentinel: the padding entries of the deterministic layout's segments (k_spmv_sweep_ordered
-// sends them to the panel's scratch slot)
-constexpr uint16_t kSweepPadRow = 0xFFFF;
-
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -358,24 +354,34 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
 }
 
-// Turn-ordered form of k_spmv_sweep_packed: the same plan, layout and gathers, but the LDS adds
-// of a workgroup are ordered. An LDS token `turn` passes from wave to wave: wave w adds the
-// products of its iteration i only when turn == i * W + w, waits for its adds to complete, then
-// hands the token on. Every row therefore receives its products in the fixed order (iteration,
-// wave, lane) that the plan alone defines, so y is bitwise the same on every run -- the
-// fixed-order accumulation of compute_results (spmv.cpp:66-104), in an order of its own -- while
-// each gather instruction still covers 64 consecutive column-sorted entries of the whole panel.
-// The token serialises only the short add phases; a wave that has handed it on issues its next
-// entry loads and gathers at once (PREF: the next iteration's entries are loaded before the
-// wait). SLEEP: s_sleep argument of the polling loop (0 = tight spin).
-template <typename V, int T, int Q, int SLEEP, bool PREF, typename A = double>
+// Deterministic form (env SPMV_SWEEP_DETERMINISTIC=1): the same plan, layout and gathers as
+// k_spmv_sweep_packed / k_spmv_sweep, but the LDS adds of a workgroup are ordered. In the default
+// kernels all 16 waves add into any row of the panel in timing order, so y changes in its last
+// bits from run to run. Here an LDS token `turn` passes from wave to wave: wave w adds the
+// products of its iteration i only when turn == i * W + w, then hands the token on. Every row
+// therefore receives its products in the order (iteration, wave, lane) that the plan alone
+// defines, and y is bitwise the same on every run and for every plan built from the same CSR --
+// the fixed-order accumulation of compute_results (spmv.cpp:66-104), in an order of its own --
+// while each gather instruction still covers 64 consecutive column-sorted entries of the whole
+// panel (the x-line sharing of the default form).
+// The token serialises only the short add phases. Each step i issues the gathers of i + 2 and
+// the entry loads of i + 4 before it waits for the token, so two iterations of gathers stay in
+// flight while the waves take turns (the loop body is unrolled 6 times -- 2 entry buffers x 3
+// gathered buffers -- so that no register with a load in flight is ever copied).
+// ORD = 1: the token store follows the adds' issue (compiler ordering only): the LDS executes a
+// CU's requests in arrival order and each wave's in program order, so the next wave, which can
+// only issue its adds after it has read the token, adds after. ORD = 0: the adds complete
+// (lgkmcnt 0) before a release store (3 % slower, profiles/r02_ab_variants.jsonl r02w).
+// PK: packed 12-byte entries (rc + chunk base); otherwise the 14-byte form (s_col, s_row).
+template <typename V, int T, int Q, bool PK, int ORD, typename A = double>
 __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
-    const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
-    const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
-    const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
-    A *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
+    const uint32_t *__restrict__ col, const uint32_t *__restrict__ cbase, const uint16_t *__restrict__ srow16,
+    const V *__restrict__ val, const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
+    const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit, A *__restrict__ part,
+    uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
     constexpr uint32_t W = T / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     A *ylds = reinterpret_cast<A *>(smem);
@@ -394,178 +400,113 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane2 = 2u * (threadIdx.x & 63);
     const uint64_t last_chunk = e1 > e0 ? e1 - 128 : e0;
-    u32x2 w[Q];
-    uint32_t cb[Q];
-    V v[Q][2];
-    bool ok[Q];
-    auto load = [&](uint64_t base, u32x2 (&w_)[Q], uint32_t (&cb_)[Q], V (&v_)[Q][2], bool (&ok_)[Q]) {
+    struct EB {  // entries of one iteration
+        u32x2 w[Q];      // packed rc words, or absolute columns
+        uint32_t cb[Q];  // chunk bases (packed form)
+        u16x2 r[Q];      // rows in the panel (14-byte form)
+        V v[Q][2];
+        bool ok[Q];
+    };
+    struct DB {  // gathered x, values and LDS slots of one iteration
+        V x[Q][2], v[Q][2];
+        uint32_t r[2 * Q];
+    };
+    auto ld = [&](uint64_t base, EB &e) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             uint64_t wbase = base + q * kGroup + 128ull * wave;
-            ok_[q] = wbase < e1;  // wave-uniform; a group past the end re-reads the last chunk
-            wbase = ok_[q] ? wbase : last_chunk;
-            const uint64_t e = wbase + lane2;
-            w_[q] = lds_<true>(reinterpret_cast<const u32x2 *>(rc + e));
-            cb_[q] = cbase[wbase >> 7];
-            loadv<true, 2>(val, e, v_[q]);
+            e.ok[q] = wbase < e1;  // wave-uniform; a group past the end re-reads the last chunk
+            wbase = e.ok[q] ? wbase : last_chunk;
+            const uint64_t ei = wbase + lane2;
+            e.w[q] = lds_<true>(reinterpret_cast<const u32x2 *>(col + ei));
+            if constexpr (PK)
+                e.cb[q] = cbase[wbase >> 7];
+            else
+                e.r[q] = lds_<true>(reinterpret_cast<const u16x2 *>(srow16 + ei));
+            loadv<true, 2>(val, ei, e.v[q]);
         }
     };
-    if constexpr (PREF)
-        load(e0, w, cb, v, ok);
-    uint32_t my = wave;  // token value of this wave's current iteration
-    for (uint64_t base = e0; base < e1; base += kStep, my += W) {
-        if constexpr (!PREF)
-            load(base, w, cb, v, ok);
-        V xv[Q][2];
+    auto gat = [&](const EB &e, DB &d) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            xv[q][0] = x[cb[q] + (w[q].x & 0xFFFFu)];
-            xv[q][1] = x[cb[q] + (w[q].y & 0xFFFFu)];
+            if constexpr (PK) {
+                d.x[q][0] = x[e.cb[q] + (e.w[q].x & 0xFFFFu)];
+                d.x[q][1] = x[e.cb[q] + (e.w[q].y & 0xFFFFu)];
+                d.r[2 * q] = e.ok[q] ? (e.w[q].x >> 16) : R;
+                d.r[2 * q + 1] = e.ok[q] ? (e.w[q].y >> 16) : R;
+            } else {
+                d.x[q][0] = x[e.w[q].x];
+                d.x[q][1] = x[e.w[q].y];
+                d.r[2 * q] = e.ok[q] ? (uint32_t)e.r[q].x : R;
+                d.r[2 * q + 1] = e.ok[q] ? (uint32_t)e.r[q].y : R;
+            }
+            d.v[q][0] = e.v[q][0];
+            d.v[q][1] = e.v[q][1];
         }
-        uint32_t ri[2 * Q];
-        V vc[Q][2];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            ri[2 * q] = ok[q] ? (w[q].x >> 16) : R;
-            ri[2 * q + 1] = ok[q] ? (w[q].y >> 16) : R;
-            vc[q][0] = v[q][0];
-            vc[q][1] = v[q][1];
-        }
-        if constexpr (PREF)
-            load(base + kStep, w, cb, v, ok);  // next iteration (past the end: the last chunk, unused)
+    };
+    auto step = [&](uint64_t base, uint32_t my, EB &e, const DB &cur, DB &fill) {
+        gat(e, fill);             // gathers of i + 2
+        ld(base + 4 * kStep, e);  // entries of i + 4 (past the end: the last chunk, unused)
         A pv[2 * Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            pv[2 * q] = A(vc[q][0]) * A(xv[q][0]);
-            pv[2 * q + 1] = A(vc[q][1]) * A(xv[q][1]);
+            pv[2 * q] = A(cur.v[q][0]) * A(cur.x[q][0]);
+            pv[2 * q + 1] = A(cur.v[q][1]) * A(cur.x[q][1]);
         }
-        // wait for the token, add, let the adds complete, hand the token on
-        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) !=
-               my) {
-            if constexpr (SLEEP > 0)
-                __builtin_amdgcn_s_sleep(SLEEP);
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != my) {
         }
-        lds_add_n<2 * Q>(ylds, ri, pv);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's adds are done
-        if ((threadIdx.x & 63) == 0)
-            __hip_atomic_store(&turn, my + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_add_n<2 * Q>(ylds, cur.r, pv);
+        if constexpr (ORD == 0) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's adds are done
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_store(&turn, my + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // compiler order only: adds, then the store
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_store(&turn, my + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
+    // 32-bit scalar trip count: all waves of the workgroup take the same number of steps. An
+    // empty unit (no entries at all: the prologue's loads would read past a 4-entry allocation)
+    // only writes its zeros.
+    const uint32_t nit = (uint32_t)((e1 - e0 + kStep - 1) / kStep);
+    if (nit == 0) {
+        __syncthreads();
+        write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
+        return;
     }
+    EB ea, eb;
+    DB d0, d1, d2;
+    ld(e0, ea);
+    ld(e0 + kStep, eb);
+    gat(ea, d0);
+    ld(e0 + 2 * kStep, ea);
+    gat(eb, d1);
+    ld(e0 + 3 * kStep, eb);
+    uint32_t my = wave;
+    uint64_t base = e0;
+    uint32_t it = 0;
+#define TSTEP(E, C, F)       \
+    step(base, my, E, C, F); \
+    base += kStep;           \
+    my += W;                 \
+    if (++it >= nit)         \
+        break;
+    while (it < nit) {
+        TSTEP(ea, d0, d2)
+        TSTEP(eb, d1, d0)
+        TSTEP(ea, d2, d1)
+        TSTEP(eb, d0, d2)
+        TSTEP(ea, d1, d0)
+        TSTEP(eb, d2, d1)
+    }
+#undef TSTEP
     __syncthreads();
     write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
 }
 
-// Deterministic form (env SPMV_SWEEP_DETERMINISTIC=1). The default kernel lets all 16 waves add
-// into any row of the panel, so a row's products land in timing order and y changes in its
-// last bits from run to run. Here each panel's rows are cut into T/64 nnz-balanced segments, one
-// per wave, and each segment has its own column-sorted, chunk-padded entries: a row's products
-// are added by its one wave, in the fixed order of its entries (the fixed-order accumulation of
-// compute_results, spmv.cpp:66-104, though not the same order), so y is the same bits on every
-// run. The waves still sweep the columns together (loose synchronisation, LAG iterations), but
-// each gather instruction covers 64 entries of one wave's rows only, so fewer lanes share an x
-// line than in the default form.
-// PK: packed entries (rc = row << 16 | column offset, one base per 32 entries); otherwise the
-// 14-byte form (s_col u32, s_row u16, value) of segments too sparse for 16-bit offsets.
-template <typename V, int T, int Q, int LAG, bool PK, typename A = double>
-__global__ __launch_bounds__(T) void k_spmv_sweep_ordered(
-    const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const uint16_t *__restrict__ srow16,
-    const V *__restrict__ val, const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ seg_row,
-    const uint32_t *__restrict__ seg_ent, const V *__restrict__ x, V *__restrict__ y)
-{
-    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    constexpr uint32_t W = T / 64;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    A *ylds = reinterpret_cast<A *>(smem);
-    __shared__ uint32_t progress[W];
-    const uint32_t p = blockIdx.x;
-    const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane2 = 2u * (threadIdx.x & 63);
-    const uint64_t e0 = seg_ent[p * W + wave], e1 = seg_ent[p * W + wave + 1];
-    const uint32_t roff = seg_row[p * W + wave] - r0;  // the wave's first row inside the panel
-    const bool hi_half = (threadIdx.x & 63) >= 32;
-    for (uint32_t i = threadIdx.x; i <= R; i += T)
-        ylds[i] = A(0);
-    if (threadIdx.x < W)
-        progress[threadIdx.x] = 0;
-    __syncthreads();
-    uint32_t iter = 0;
-    const uint64_t last_chunk = e1 > e0 ? e1 - 128 : e0;
-    for (uint64_t base = e0; base < e1; base += Q * 128ull) {
-        u32x2 w[Q];
-        uint32_t cb[Q][2];
-        V v[Q][2];
-        bool ok[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            uint64_t wbase = base + 128ull * q;  // this wave's own consecutive chunks
-            ok[q] = wbase < e1;                  // wave-uniform
-            wbase = ok[q] ? wbase : last_chunk;
-            const uint64_t e = wbase + lane2;
-            w[q] = lds_<true>(reinterpret_cast<const u32x2 *>(rc + e));
-            if constexpr (PK) {
-                // one base per 32 entries: gather instruction j covers logical entries 64j + lane,
-                // i.e. quarters 2j (lanes 0-31) and 2j + 1 (lanes 32-63); four scalar loads per chunk
-                const uint32_t *b4 = cbase + (wbase >> 5);
-                const uint32_t b0 = b4[0], b1 = b4[1], b2 = b4[2], b3 = b4[3];
-                cb[q][0] = hi_half ? b1 : b0;
-                cb[q][1] = hi_half ? b3 : b2;
-            } else {  // absolute columns in w, rows from s_row
-                const u16x2 r2 = lds_<true>(reinterpret_cast<const u16x2 *>(srow16 + e));
-                cb[q][0] = r2.x;
-                cb[q][1] = r2.y;
-            }
-            loadv<true, 2>(val, e, v[q]);
-        }
-        V xv[Q][2];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if constexpr (PK) {
-                xv[q][0] = x[cb[q][0] + (w[q].x & 0xFFFFu)];
-                xv[q][1] = x[cb[q][1] + (w[q].y & 0xFFFFu)];
-            } else {
-                xv[q][0] = x[w[q].x];
-                xv[q][1] = x[w[q].y];
-            }
-        }
-        uint32_t ri[2 * Q];
-        A pv[2 * Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const uint32_t a = PK ? w[q].x >> 16 : cb[q][0], b = PK ? w[q].y >> 16 : cb[q][1];
-            ri[2 * q] = ok[q] && a != kSweepPadRow ? a + roff : R;
-            ri[2 * q + 1] = ok[q] && b != kSweepPadRow ? b + roff : R;
-            pv[2 * q] = A(v[q][0]) * A(xv[q][0]);
-            pv[2 * q + 1] = A(v[q][1]) * A(xv[q][1]);
-        }
-        lds_add_n<2 * Q>(ylds, ri, pv);
-        ++iter;
-        if ((threadIdx.x & 63) == 0)
-            __hip_atomic_store(&progress[wave], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        for (;;) {  // wait while more than LAG iterations ahead of the slowest unfinished wave
-            const uint32_t lane = threadIdx.x & 63;
-            uint32_t pr = lane < W ? __hip_atomic_load(&progress[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                                   : 0xFFFFFFFFu;
-#pragma unroll
-            for (int d = 1; d < (int)W; d <<= 1) {
-                const uint32_t o = __shfl_xor(pr, d, 64);
-                pr = o < pr ? o : pr;
-            }
-            if (__builtin_amdgcn_readfirstlane(pr) + LAG >= iter)
-                break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    // a finished wave never holds the others back
-    if ((threadIdx.x & 63) == 0)
-        __hip_atomic_store(&progress[wave], 0xFFFFFFFFu - LAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < R; i += T)
-        y[r0 + i] = V(ylds[i]);
-}
-
-// group c of G entries (a 128-entry chunk, or half a chunk = one gather instruction in the
-// deterministic form): base = min column; fails the plan's packing when the span >= 65536
+// group c of G entries (a 128-entry chunk): base = min column; fails the plan's packing when the
+// span >= 65536
 __global__ void k_sweep_chunk_base(const uint32_t *__restrict__ col, uint64_t nchunks, uint32_t G,
                                    uint32_t *__restrict__ cbase, uint32_t *__restrict__ bad)
 {
@@ -667,8 +608,7 @@ __global__ void k_sweep_scatter(const uint32_t *__restrict__ keys, const uint32_
 template <typename V>
 __global__ void k_sweep_pad(uint32_t npanels, const uint32_t *__restrict__ panel_row,
                             const uint32_t *__restrict__ off, const uint32_t *__restrict__ poff,
-                            uint32_t *__restrict__ s_col, uint16_t *__restrict__ s_row, V *__restrict__ s_val,
-                            bool sentinel)
+                            uint32_t *__restrict__ s_col, uint16_t *__restrict__ s_row, V *__restrict__ s_val)
 {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npanels)
@@ -678,7 +618,7 @@ __global__ void k_sweep_pad(uint32_t npanels, const uint32_t *__restrict__ panel
     const uint32_t pad_col = first_pad > poff[p] ? s_col[first_pad - 1] : 0u;
     for (uint64_t d = first_pad; d < poff[p + 1]; ++d) {
         s_col[d] = pad_col;  // value 0: adds nothing; column kept near the panel's last one
-        s_row[d] = sentinel ? kSweepPadRow : (uint16_t)R;  // scratch slot, never written back
+        s_row[d] = (uint16_t)R;  // scratch slot, never written back
         s_val[d] = V(0);
     }
 }
@@ -719,17 +659,21 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT, A>, grid, block, lds, s, p.d_s_col,   \
                        p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, d_x, d_y)
-    if (p.sweep_det) {  // deterministic form
-        if (p.sweep_packed)
-            launch_or_warm(warm, k_spmv_sweep_ordered<ValueType, T, 2, 2, true, A>, grid, block, lds, s, p.d_s_col,
-                           p.d_s_cbase, (const uint16_t *)nullptr, p.d_s_val, p.d_panel_row, p.d_seg_row,
-                           p.d_unit_ent, d_x, d_y);
-        else
-            launch_or_warm(warm, k_spmv_sweep_ordered<ValueType, T, 2, 2, false, A>, grid, block, lds, s, p.d_s_col,
-                           (const uint32_t *)nullptr, p.d_s_row, p.d_s_val, p.d_panel_row, p.d_seg_row,
-                           p.d_unit_ent, d_x, d_y);
+    // deterministic form (env SPMV_SWEEP_DETERMINISTIC=1, or variants 91 / 94 on any sweep plan)
+#define TURN(PK, ORD)                                                                              \
+    launch_or_warm(warm, k_spmv_sweep_turn<ValueType, T, 2, PK, ORD, A>, grid, block, lds, s, p.d_s_col,          \
+                   p.d_s_cbase, p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, \
+                   part, p.panel_rmax + 1, d_x, d_y)
+    if (p.sweep_det || p.sweep_variant == kSweepTurn || p.sweep_variant == kSweepTurnOrdered) {
+        const bool ord0 = p.sweep_variant == kSweepTurnOrdered;
+        if (p.sweep_packed) {
+            if (ord0) TURN(true, 0); else TURN(true, 1);
+        } else {
+            if (ord0) TURN(false, 0); else TURN(false, 1);
+        }
         return;
     }
+#undef TURN
     if (p.sweep_packed) {
 #define PKN(NT, Q, LAG, ABL)                                                                        \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
@@ -764,18 +708,6 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 58: PKA(7); break;  // x gathers that bypass L1 (sc1)
         case 53: PKA(10); break;  // half the value bytes: 8 B/entry streamed instead of 12
 #endif
-#define TURN(Q, SLEEP, PREF)                                                                      \
-    launch_or_warm(warm, k_spmv_sweep_turn<ValueType, T, Q, SLEEP, PREF, A>, grid, block, lds, s, p.d_s_col, \
-                   p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part,   \
-                   p.panel_rmax + 1, d_x, d_y)
-        // 70-75: turn-ordered adds (bitwise reproducible y)
-        case 70: TURN(2, 1, false); break;
-        case 71: TURN(2, 0, false); break;
-        case 72: TURN(2, 1, true); break;
-        case 73: TURN(2, 0, true); break;
-        case 74: TURN(4, 1, true); break;
-        case 75: TURN(4, 0, true); break;
-#undef TURN
         default: PK(2, 2); break;
         }
 #undef PKA
@@ -854,11 +786,10 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     cus *= 1024 / p.sweep_threads;  // resident workgroups per round
     // env SPMV_SWEEP_SPLIT: 0 = never split, 2 = split whenever >= 2 pieces fit, else heuristic
     const char *senv = std::getenv("SPMV_SWEEP_SPLIT");
-    // env SPMV_SWEEP_DETERMINISTIC=1: one segment of rows per wave (k_spmv_sweep_ordered); panels
-    // are never cut into column pieces in that form
+    // env SPMV_SWEEP_DETERMINISTIC=1: the same layout, run by k_spmv_sweep_turn (ordered adds)
     const char *denv = std::getenv("SPMV_SWEEP_DETERMINISTIC");
     const bool det = denv && denv[0] == '1';
-    const bool allow_split = !(senv && senv[0] == '0') && !det;
+    const bool allow_split = !(senv && senv[0] == '0');
     const bool force_split = senv && senv[0] == '2';
     bool split_mode = false;
     std::vector<uint32_t> prow;
@@ -896,29 +827,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         }
     }
     const uint32_t P = (uint32_t)(prow.size() - 1);
-    // sort segments: the panels, or (deterministic form) W nnz-balanced row segments per panel,
-    // each padded to whole chunks of its own
-    const uint32_t W = det ? (uint32_t)(p.sweep_threads / kWave) : 1;
-    std::vector<uint32_t> srow;
-    if (det) {
-        srow.assign(1, 0);
-        for (uint32_t q = 0; q < P; ++q) {
-            const uint64_t a = h_rp[prow[q]], b = h_rp[prow[q + 1]];
-            for (uint32_t w = 1; w < W; ++w) {
-                // the row boundary nearest to the segment's share of the panel's entries (keeps
-                // the segments' densities close: their 32-entry column groups must stay < 65536)
-                const IndexType target = (IndexType)(a + (b - a) * w / W);
-                IndexType r = (IndexType)(std::lower_bound(h_rp + prow[q], h_rp + prow[q + 1], target) - h_rp);
-                if (r > prow[q] && target - h_rp[r - 1] < h_rp[r] - target)
-                    --r;
-                r = std::min<IndexType>(std::max<IndexType>(r, srow.back()), prow[q + 1]);
-                srow.push_back(r);
-            }
-            srow.push_back(prow[q + 1]);
-        }
-    } else {
-        srow = prow;
-    }
+    const std::vector<uint32_t> &srow = prow;  // sort segments = the panels
     const uint32_t S = (uint32_t)(srow.size() - 1);
     std::vector<uint32_t> off(S + 1), poff(S + 1);
     off[0] = poff[0] = 0;
@@ -947,32 +856,26 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     const double mean = P ? double(padded) / P : 0.0;
     std::vector<uint32_t> punit(P + 1, 0);
     for (uint32_t q = 0; q < P; ++q) {
-        const uint64_t chunks = (uint64_t(poff[(q + 1) * W]) - poff[q * W]) / kSweepChunk;
+        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
         uint64_t k = split * std::max<uint64_t>(
                                  1, (uint64_t)std::ceil(double(poff[q + 1] - poff[q]) / std::max(2.0 * mean, 1.0)));
-        k = det ? 1 : std::max<uint64_t>(1, std::min<uint64_t>(k, chunks));
+        k = std::max<uint64_t>(1, std::min<uint64_t>(k, chunks));
         punit[q + 1] = punit[q] + (uint32_t)k;
     }
     const uint32_t U = punit[P];
     std::vector<uint32_t> uent, upanel(std::max<uint32_t>(U, 1));
     bool multi = false;
-    if (det) {
-        uent = poff;  // the deterministic kernel reads each wave's segment range
-        for (uint32_t q = 0; q < P; ++q)
-            upanel[q] = q;
-    } else {
-        uent.assign((size_t)U + 1, 0);
-        for (uint32_t q = 0; q < P; ++q) {
-            const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
-            const uint32_t k = punit[q + 1] - punit[q];
-            multi |= k > 1;
-            for (uint32_t t = 0; t < k; ++t) {
-                uent[punit[q] + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / k));
-                upanel[punit[q] + t] = q;
-            }
+    uent.assign((size_t)U + 1, 0);
+    for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
+        const uint32_t k = punit[q + 1] - punit[q];
+        multi |= k > 1;
+        for (uint32_t t = 0; t < k; ++t) {
+            uent[punit[q] + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / k));
+            upanel[punit[q] + t] = q;
         }
-        uent[U] = poff[P];
     }
+    uent[U] = poff[P];
     p.sweep_split = multi ? std::max<uint32_t>(split, 2) : 1;  // > 1: combine kernel needed
     p.nunits = U;
     if (multi)
@@ -994,13 +897,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     SPMV_TRY(hipMalloc((void **)&p.d_panel_row, (P + 1) * 4));
     SPMV_TRY(hipMalloc((void **)&p.d_unit_ent, uent.size() * 4));
     SPMV_TRY(hipMemcpyAsync(p.d_panel_row, prow.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
-    // rows of the sort segments (the panels themselves unless deterministic)
-    uint32_t *d_srow = p.d_panel_row;
-    if (det) {
-        SPMV_TRY(hipMalloc((void **)&p.d_seg_row, (S + 1) * 4));
-        SPMV_TRY(hipMemcpyAsync(p.d_seg_row, srow.data(), (S + 1) * 4, hipMemcpyHostToDevice, s));
-        d_srow = p.d_seg_row;
-    }
+    uint32_t *d_srow = p.d_panel_row;  // rows of the sort segments (the panels)
     SPMV_TRY(hipMemcpyAsync(p.d_unit_ent, uent.data(), uent.size() * 4, hipMemcpyHostToDevice, s));
     SPMV_TRY(hipMalloc((void **)&p.d_s_col, std::max<uint64_t>(p.ent_pad, 4) * 4));
     SPMV_TRY(hipMalloc((void **)&p.d_s_row, std::max<uint64_t>(p.ent_pad, 4) * 2));
@@ -1053,12 +950,11 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         SW_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL((k_sweep_pad<ValueType>), dim3((S + 255) / 256), dim3(256), 0, s, S, d_srow, d_off,
-                       d_poff, p.d_s_col, p.d_s_row, p.d_s_val, det);
+                       d_poff, p.d_s_col, p.d_s_row, p.d_s_val);
     SW_TRY(hipGetLastError());
-    // 12-byte packed entries when every 128-entry chunk spans < 65536 columns (deterministic
-    // form: every 32-entry quarter chunk, whose segments are W times sparser than a panel)
+    // 12-byte packed entries when every 128-entry chunk spans < 65536 columns
     {
-        const uint32_t group = det ? kSweepChunk / 4 : kSweepChunk, gshift = det ? 5 : 7;
+        const uint32_t group = kSweepChunk, gshift = 7;
         const uint64_t nchunks = p.ent_pad / group;
         SW_TRY(hipMalloc((void **)&p.d_s_cbase, std::max<uint64_t>(nchunks, 1) * 4));
         uint32_t *d_bad = d_off;  // reuse: d_off is no longer needed once the scatter ran

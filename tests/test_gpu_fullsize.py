@@ -61,3 +61,37 @@ def test_config3_and_5_powerlaw_10m_160m_auto_sweep(dtype):
     assert err <= TOL[np.dtype(dtype)], err
     if np.dtype(dtype) == np.float64:
         assert err <= 1e-12, err
+
+
+@pytest.mark.timeout(600)
+def test_config3_deterministic_sweep_bitwise_over_runs(monkeypatch):
+    """SPMV_SWEEP_DETERMINISTIC=1 on the headline matrix: ten runs and a second plan give the
+    same bits (adds in a fixed (iteration, wave, lane) order, k_spmv_sweep_turn), within the
+    fp64 tolerance of the oracle, and within 1e-13 of the default (timing-order) sweep."""
+    import torch
+    lib = spmv_hw.load(np.float64)
+    n, z = 10_000_000, 160_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
+    plans = [spmv_hw.Plan.from_device(lib, rp, col, val, n) for _ in range(2)]
+    monkeypatch.delenv("SPMV_SWEEP_DETERMINISTIC")
+    fast = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    y0 = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plans[0].run(x, y0)
+    y = torch.empty_like(y0)
+    for k in range(10):
+        y.fill_(float("nan"))
+        plans[k % 2].run(x, y)
+        assert torch.equal(y.view(torch.int64), y0.view(torch.int64)), f"run {k} differs"
+    fast.run(x, y)
+    torch.cuda.synchronize()
+    rel = float(((y - y0).abs().max() / y0.abs().max()).item())
+    assert rel < 1e-13, rel
+    for p in plans + [fast]:
+        p.destroy()
+    h_rp = rp.cpu().numpy().view(np.uint32)
+    h_col = col.cpu().numpy().view(np.uint32)
+    h_val, h_x, h_y = val.cpu().numpy(), x.cpu().numpy(), y0.cpu().numpy()
+    ref = oracle.spmv_gold(h_rp, h_col, h_val, h_x)
+    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, h_y) <= 1e-12

@@ -47,7 +47,7 @@ def kernel(request, monkeypatch):
         monkeypatch.setenv("SPMV_TILE_NARROW", "0")
     if request.param == "sweep_unpacked":
         monkeypatch.setenv("SPMV_SWEEP_PACKED", "0")
-    if request.param == "sweep_det":  # deterministic sweep: one row segment per wave
+    if request.param == "sweep_det":  # deterministic sweep: LDS adds in a fixed (iteration, wave) order
         monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
     if request.param == "slices_wide":
         monkeypatch.setenv("SPMV_SLICE_NARROW", "0")
