@@ -832,7 +832,7 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
 #ifndef SPMV_ABLATIONS
     // the measurement-only ablations (some give a wrong y by design) exist only in the tools
     // library built with -DSPMV_ABLATIONS (Makefile target `ablations`, tools/ab_variants.py)
-    if ((p->kernel == kKernelSweep && variant >= 53 && variant <= 63) || (p->kernel == kKernelBlocked && variant == 1)) {
+    if ((p->kernel == kKernelSweep && variant >= 51 && variant <= 63) || (p->kernel == kKernelBlocked && variant == 1)) {
         set_error("spmv_plan_set_variant: measurement-only ablation variant (tools library only)");
         return 1;
     }

@@ -386,6 +386,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     A *ylds = reinterpret_cast<A *>(smem);
     __shared__ uint32_t turn;
+    __shared__ uint32_t progress[W];  // ORD 2 only
     const uint32_t p = unit_panel[blockIdx.x];
     const uint32_t pieces = panel_unit[p + 1] - panel_unit[p];
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
@@ -394,6 +395,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
         ylds[i] = A(0);
     if (threadIdx.x == 0)
         turn = 0;
+    if (threadIdx.x < W)
+        progress[threadIdx.x] = 0;
     __syncthreads();
     constexpr uint64_t kGroup = 2ull * T;
     constexpr uint64_t kStep = Q * kGroup;
@@ -453,6 +456,28 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
             pv[2 * q] = A(cur.v[q][0]) * A(cur.x[q][0]);
             pv[2 * q + 1] = A(cur.v[q][1]) * A(cur.x[q][1]);
         }
+        if constexpr (ORD >= 2) {  // measurement only: unordered adds (2: waves at most 2 steps apart)
+            lds_add_n<2 * Q>(ylds, cur.r, pv);
+            if constexpr (ORD == 2) {
+                const uint32_t iter = my / W + 1;
+                if ((threadIdx.x & 63) == 0)
+                    __hip_atomic_store(&progress[wave], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (;;) {
+                    const uint32_t lane = threadIdx.x & 63;
+                    uint32_t pr = lane < W ? __hip_atomic_load(&progress[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                           : 0xFFFFFFFFu;
+#pragma unroll
+                    for (int d = 1; d < (int)W; d <<= 1) {
+                        const uint32_t o = __shfl_xor(pr, d, 64);
+                        pr = o < pr ? o : pr;
+                    }
+                    if (__builtin_amdgcn_readfirstlane(pr) + 2 >= iter)
+                        break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            return;
+        }
         while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != my) {
         }
         lds_add_n<2 * Q>(ylds, cur.r, pv);
@@ -501,6 +526,9 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
         TSTEP(eb, d2, d1)
     }
 #undef TSTEP
+    if constexpr (ORD == 2)  // a finished wave never holds the others back
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_store(&progress[wave], 0xFFFFFFF0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __syncthreads();
     write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
 }
@@ -664,6 +692,17 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep_turn<ValueType, T, 2, PK, ORD, A>, grid, block, lds, s, p.d_s_col,          \
                    p.d_s_cbase, p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, \
                    part, p.panel_rmax + 1, d_x, d_y)
+#ifdef SPMV_ABLATIONS
+    // measurement only: the turn kernel's pipeline without the ordering (52: loose sync, 51: none)
+    if (p.sweep_packed && p.sweep_variant == 52) {
+        TURN(true, 2);
+        return;
+    }
+    if (p.sweep_packed && p.sweep_variant == 51) {
+        TURN(true, 3);
+        return;
+    }
+#endif
     if (p.sweep_det || p.sweep_variant == kSweepTurn || p.sweep_variant == kSweepTurnOrdered) {
         const bool ord0 = p.sweep_variant == kSweepTurnOrdered;
         if (p.sweep_packed) {

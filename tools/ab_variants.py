@@ -52,7 +52,7 @@ def main():
     a = ap.parse_args()
     # measurement-only ablations live in the tools library only (spmv-fpga_amd Makefile target
     # `ablations`); the product library refuses them
-    abl = any((v.split(":")[0].startswith("sweep") and int(v.split(":")[1]) >= 53)
+    abl = any((v.split(":")[0].startswith("sweep") and int(v.split(":")[1]) in range(51, 64))
               or (v.split(":")[0].startswith("blocked") and v.split(":")[1] == "1")
               for v in a.variants.split(",") if ":" in v)
     if abl:
