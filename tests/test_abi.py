@@ -250,3 +250,15 @@ def test_measurement_ablations_are_not_in_the_product_library_symbols(dtype):
     for ln in blocked:  # <V, VF, XLDS, ABL>
         args = ln.split("k_blocked_partials<", 1)[1].split(">", 1)[0].split(", ")
         assert args[3] == "0", ln
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_deterministic_kernel_ships_only_its_ordered_forms(dtype):
+    """k_spmv_sweep_turn<V, T, Q, PK, ORD, A>: the product library holds ORD 0 and 1 (ordered
+    adds); ORD 2 / 3 (the same pipeline without ordering, ablations 51 / 52) exist only in the
+    tools library."""
+    out = subprocess.run(["nm", "-C", spmv_hw.lib_path(dtype)], capture_output=True, text=True, check=True).stdout
+    turns = [ln for ln in out.splitlines() if "k_spmv_sweep_turn<" in ln]
+    assert turns
+    ords = {ln.split("k_spmv_sweep_turn<", 1)[1].split(">", 1)[0].split(", ")[4] for ln in turns}
+    assert ords == {"0", "1"}, ords
