@@ -32,8 +32,10 @@ cpu_baseline (the oracle's restatement of spmv_gold, 1 thread, on the host of th
 parity (full-size componentwise-scaled error vs that oracle run),
 lds_xtiles (power-law, 1 GPU: the same matrix through kernel 4, the reference's dataflow with a
 block of x in LDS per workgroup -- the technique BASELINE configs 3/5 name -- timed beside the
-headline kernel), side_configs (1 GPU: BASELINE config 2, banded 1M x 16 fp64, and config 5, the
-power-law matrix in fp32, each timed the same way with its own roofline and oracle parity).
+headline kernel), deterministic (power-law, 1 GPU: the same matrix with SPMV_SWEEP_DETERMINISTIC=1,
+bitwise reproducible y, timed the same way), side_configs (1 GPU: BASELINE config 2, banded
+1M x 16 fp64, and config 5, the power-law matrix in fp32, each timed the same way with its own
+roofline and oracle parity).
 """
 from __future__ import annotations
 
@@ -69,6 +71,8 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="default: strong (config 4) when --gpus > 1, weak (= single GPU) otherwise")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
+    ap.add_argument("--no-det", action="store_true",
+                    help="skip the deterministic-sweep side line (SPMV_SWEEP_DETERMINISTIC=1)")
     ap.add_argument("--no-xtiles", action="store_true",
                     help="skip the LDS x-tile (kernel 4, blocked) measurement beside the headline")
     ap.add_argument("--no-strong-companion", action="store_true",
@@ -242,6 +246,45 @@ def lds_xtiles(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
            "device_bytes": st["device_bytes"], "max_rel_diff_vs_value_kernel": diff}
     plan.destroy()
     del y
+    torch.cuda.empty_cache()
+    return res
+
+
+def deterministic_side(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
+    """The same matrix with SPMV_SWEEP_DETERMINISTIC=1 (k_spmv_sweep_turn: LDS adds in a fixed
+    (iteration, wave, lane) order on the default layout), timed like the headline; y must be the
+    same bits over the timed runs and a fresh run, and within 1e-13 of the headline's y."""
+    saved = os.environ.get("SPMV_SWEEP_DETERMINISTIC")
+    os.environ["SPMV_SWEEP_DETERMINISTIC"] = "1"
+    try:
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, ncols, device=dev_index, stream=stream)
+    finally:
+        if saved is None:
+            os.environ.pop("SPMV_SWEEP_DETERMINISTIC", None)
+        else:
+            os.environ["SPMV_SWEEP_DETERMINISTIC"] = saved
+    y0 = torch.empty_like(y_ref)
+    plan.run(x, y0, stream)
+    y = torch.empty_like(y_ref)
+    for _ in range(args.warmup):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    for _ in range(args.steps):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    ms, _, launches = plan.timing()
+    plan.set_timing(False)
+    itype = torch.int64 if y.element_size() == 8 else torch.int32
+    bitwise = bool(torch.equal(y.view(itype), y0.view(itype)))
+    diff = float(((y.double() - y_ref.double()).abs().max() / y_ref.double().abs().max().clamp_min(1e-300)).item())
+    st = plan.stats()
+    res = {"kernel": "k_spmv_sweep_turn", "env": "SPMV_SWEEP_DETERMINISTIC=1", "ms_per_step": round(ms, 5),
+           "launches": launches, "gflops": round(2.0 * st["nr_nzeros"] / (ms * 1e-3) / 1e9, 3),
+           "alg_GBps": round(st["algorithmic_bytes"] / (ms * 1e-3) / 1e9, 2),
+           "bitwise_over_runs": bitwise, "max_rel_diff_vs_value_kernel": diff}
+    plan.destroy()
+    del y, y0
     torch.cuda.empty_cache()
     return res
 
@@ -498,9 +541,11 @@ def main():
     graph = {"iters": args.steps, "ms_per_step": round(ms, 5), "timed": "headline (value, ms_per_step)",
              "eager_ms_per_step": round(eager_ms, 5)}
 
-    xtiles = None
+    xtiles = det = None
     if want_xtiles:
         xtiles = lds_xtiles(lib, args, rp, col, val, x, y, ncols, local, stream)
+        if not args.no_det:
+            det = deterministic_side(lib, args, rp, col, val, x, y, ncols, local, stream)
         if not keep_csr:
             del rp, col, val
             torch.cuda.empty_cache()
@@ -690,6 +735,7 @@ def main():
             "strong_companion": strong,
             "weak_companion": weak,
             "lds_xtiles": xtiles,
+            "deterministic": det,
             "side_configs": side,
             "host_copy": host,
             "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
