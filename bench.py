@@ -43,6 +43,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -71,6 +72,9 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="default: strong (config 4) when --gpus > 1, weak (= single GPU) otherwise")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
+    ap.add_argument("--extras-timeout", type=float, default=420.0,
+                    help="seconds the reported-only fields after the measurement may take before the "
+                         "line is printed without them")
     ap.add_argument("--no-det", action="store_true",
                     help="skip the deterministic-sweep side line (SPMV_SWEEP_DETERMINISTIC=1)")
     ap.add_argument("--no-xtiles", action="store_true",
@@ -542,10 +546,16 @@ def main():
              "eager_ms_per_step": round(eager_ms, 5)}
 
     xtiles = det = None
-    if want_xtiles:
-        xtiles = lds_xtiles(lib, args, rp, col, val, x, y, ncols, local, stream)
+    if want_xtiles:  # reported beside the headline, never fatal to it
+        try:
+            xtiles = lds_xtiles(lib, args, rp, col, val, x, y, ncols, local, stream)
+        except Exception as e:
+            xtiles = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
         if not args.no_det:
-            det = deterministic_side(lib, args, rp, col, val, x, y, ncols, local, stream)
+            try:
+                det = deterministic_side(lib, args, rp, col, val, x, y, ncols, local, stream)
+            except Exception as e:
+                det = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
         if not keep_csr:
             del rp, col, val
             torch.cuda.empty_cache()
@@ -635,8 +645,69 @@ def main():
               "src": "TCC_HIT_sum+TCC_MISS_sum (profiles/traffic.json) / kernel_ms; peak = "
                      "L2-resident gather rate (profiles/r01_hbm_calib.jsonl)"}
 
-    exchange = None
-    if world > 1:
+    out = {
+        "metric": "SpMV GFLOP/s + effective HBM GB/s (% roofline), fp64, 1/2/4/8 MI355X",
+        "value": round(gflops, 3),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 5),
+        "higher_is_better": True,
+        "scaling": args.scaling if world > 1 else "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (splitmix64 generator, SURVEY.md §8d)",
+        "config": dict(desc, parallelism=f"row-slice x{world}", dtype=args.dtype),
+        "effective_GBps": round(eff_gbps, 2),
+        "roofline_pct": round(100.0 * eff_gbps / (HBM_PEAK_GBPS * world), 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                     "peak_measured": stream_peak,
+                     "frac_of_measured": round(achieved / stream_peak, 4) if stream_peak else None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "kernel": kname, "kernel_ms": round(kernel_ms, 5), "l2": l2,
+                     "kernel_launches": launches, "alg_bytes_per_launch": alg_local},
+        "cpu_baseline": None,
+        "parity": None,
+        "exchange": None,
+        "graph": graph,
+        "strong_companion": None,
+        "weak_companion": None,
+        "lds_xtiles": xtiles,
+        "deterministic": det,
+        "side_configs": None,
+        "host_copy": host,
+        "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
+        "setup_s": round(setup_s, 2),
+    }
+    # the line above is complete; what follows adds reported-only fields. Each runs under a
+    # try (reported, never fatal), and a watchdog prints the line as it stands and ends the
+    # process if they take longer than --extras-timeout seconds (a hung collective on an
+    # 8-GPU node must not cost the measured value)
+    emitted = threading.Event()
+
+    def emit(note=None):
+        if rank == 0 and not emitted.is_set():
+            emitted.set()
+            line = dict(out, extras_timeout=note) if note else out
+            print(json.dumps(line), flush=True)
+
+    def on_timeout():
+        emit(f"extras still running after {args.extras_timeout} s; line printed without them")
+        sys.stdout.flush()
+        os._exit(0)
+
+    watchdog = threading.Timer(args.extras_timeout, on_timeout)
+    watchdog.daemon = True
+    watchdog.start()
+
+    def guarded(field, fn):
+        try:
+            out[field] = fn()
+        except Exception as e:  # reported, never fatal to the bench line
+            out[field] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+
+    def exchange_fields():
         cnt = [0.0] * world
         cnt[rank] = float(st["nr_rows"])
         counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
@@ -685,63 +756,25 @@ def main():
                 res["native"] = native_exchange(lib, plan, x, st["nr_cols"], counts, world, rank, dev)
             except Exception as e:  # reported, never fatal to the bench line
                 res["native"] = {"error": str(e)[:300]}
-        exchange = res
+        return res
 
-    strong = None
+    if world > 1:
+        guarded("exchange", exchange_fields)
     if world > 1 and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
-        strong = strong_companion(lib, args, world, rank, dev, stream)
-    weak = None
+        guarded("strong_companion", lambda: strong_companion(lib, args, world, rank, dev, stream))
     if world > 1 and args.scaling == "strong" and args.workload == "powerlaw" and not args.no_weak_companion:
-        weak = weak_companion(lib, args, world, rank, dev, stream)
-
-    cpu = None
-    parity = None
+        guarded("weak_companion", lambda: weak_companion(lib, args, world, rank, dev, stream))
     if keep_csr:
-        cpu, parity = cpu_baseline(lib, rp, col, val, x, y, args.cpu_reps, args.cpu_threads)
+        def cpu_fields():
+            out["cpu_baseline"], out["parity"] = cpu_baseline(lib, rp, col, val, x, y, args.cpu_reps, args.cpu_threads)
+            return out["cpu_baseline"]
+        guarded("cpu_baseline", cpu_fields)
         del rp, col, val
         torch.cuda.empty_cache()
-
-    side = None
     if world == 1 and args.workload == "powerlaw" and args.dtype == "f64" and not args.no_side_configs:
-        side = {name: side_config(args, name, dev, stream) for name in ("config2", "config5")}
-
-    if rank == 0:
-        out = {
-            "metric": "SpMV GFLOP/s + effective HBM GB/s (% roofline), fp64, 1/2/4/8 MI355X",
-            "value": round(gflops, 3),
-            "unit": "GFLOP/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 5),
-            "higher_is_better": True,
-            "scaling": args.scaling if world > 1 else "weak",
-            "vs_baseline": None,
-            "dtype": args.dtype,
-            "data": "synthetic (splitmix64 generator, SURVEY.md §8d)",
-            "config": dict(desc, parallelism=f"row-slice x{world}", dtype=args.dtype),
-            "effective_GBps": round(eff_gbps, 2),
-            "roofline_pct": round(100.0 * eff_gbps / (HBM_PEAK_GBPS * world), 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                         "peak_measured": stream_peak,
-                         "frac_of_measured": round(achieved / stream_peak, 4) if stream_peak else None,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": kname, "kernel_ms": round(kernel_ms, 5), "l2": l2,
-                         "kernel_launches": launches, "alg_bytes_per_launch": alg_local},
-            "cpu_baseline": cpu,
-            "parity": parity,
-            "exchange": exchange,
-            "graph": graph,
-            "strong_companion": strong,
-            "weak_companion": weak,
-            "lds_xtiles": xtiles,
-            "deterministic": det,
-            "side_configs": side,
-            "host_copy": host,
-            "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
-            "setup_s": round(setup_s, 2),
-        }
-        print(json.dumps(out), flush=True)
+        guarded("side_configs", lambda: {name: side_config(args, name, dev, stream) for name in ("config2", "config5")})
+    watchdog.cancel()
+    emit()
     plan.destroy()
     if world > 1:
         dist.destroy_process_group()
