@@ -331,7 +331,8 @@ def side_config(args, name, dev, stream):
     err = oracle.scaled_error(r, c, h[2], h[3], ref, y.cpu().numpy())
     tol = 1e-6 if dtype == np.float64 else 1e-4
     alg = st["algorithmic_bytes"]
-    names = {0: "k_spmv_tiles", 2: "k_spmv_sweep_packed" if st["format"] & 2 else "k_spmv_sweep", 5: "k_spmv_slices"}
+    names = {0: "k_spmv_tiles", 2: "k_spmv_sweep_packed" if st["format"] & 2 else "k_spmv_sweep", 5: "k_spmv_slices",
+             6: "k_bin_mul + k_bin_acc"}
     res = {"config": desc, "ms_per_step": round(wall_ms, 5), "kernel_ms": round(kernel_ms, 5),
            "gflops": round(2.0 * st["nr_nzeros"] / (wall_ms * 1e-3) / 1e9, 3),
            "effective_GBps": round(alg / (wall_ms * 1e-3) / 1e9, 2),
@@ -602,6 +603,8 @@ def main():
         kname = "k_blocked_partials"
     elif st["kernel"] == 5:
         kname = "k_spmv_slices"
+    elif st["kernel"] == 6:
+        kname = "k_bin_mul + k_bin_acc"
     else:
         kname = "k_spmv_tiles"
     traffic = None

@@ -203,7 +203,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         spmv_plan_stats st;
         spmv_plan_get_stats(h->plan, &st);
         const spmv_plan &pl = *h->plan;
-        const bool sweep = pl.kernel == kKernelSweep;
+        const bool sweep = pl.kernel == kKernelSweep || pl.kernel == kKernelBinned;
         const bool slices = pl.kernel == kKernelSlices;
         // stored entries of the representation (padded for tiles, sweep and slices, plain for
         // gold / FPGA order / blocked)
@@ -213,7 +213,8 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
                                                             : pl.nnz_pad;
         const uint64_t val_bytes = stored * sizeof(ValueType);
         // the index stream of the unit's representation (opaque device address)
-        h->sub[0] = sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)
+        h->sub[0] = pl.kernel == kKernelBinned ? reinterpret_cast<BusDataType *>(pl.d_b_colw)
+                    : sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)
                     : (slices || pl.kernel == kKernelBlocked || pl.tile_col_bytes < 4)
                         ? reinterpret_cast<BusDataType *>(pl.d_colnar)
                         : reinterpret_cast<BusDataType *>(pl.d_col);

@@ -112,6 +112,8 @@ static int requested_kernel()
         return kKernelBlocked;
     if (!std::strcmp(e, "slices"))
         return kKernelSlices;
+    if (!std::strcmp(e, "binned"))
+        return kKernelBinned;
     return -1;
 }
 
@@ -365,6 +367,16 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
                         const IndexType *d_col, const ValueType *d_val, hipStream_t s)
 {
     P.kernel = kernel;
+    if (kernel == kKernelBinned) {
+        // rc 2: the (window, panel) segment table is too large; automatic plans take the sweep
+        const int rc = build_binned(P, h_row_ptr, d_col, d_val, s);
+        if (rc == 2 && automatic) {
+            P.kernel = kernel = kKernelSweep;
+            (void)hipGetLastError();
+        } else if (rc) {
+            return 1;
+        }
+    }
     if (kernel == kKernelSweep || kernel == kKernelSlices) {
         // rc 2: the layout cannot hold this matrix (32-bit entry offsets, or the automatic
         // choice's padding limit); automatic plans fall back to the tiles, which have neither
@@ -375,7 +387,7 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
         else if (rc)
             return 1;
     }
-    if (kernel == kKernelSweep || kernel == kKernelSlices) {
+    if (kernel == kKernelSweep || kernel == kKernelSlices || kernel == kKernelBinned) {
         // built above
     } else if (kernel == kKernelBlocked) {
         if (fpga_params(P) || build_blocked(P, h_row_ptr, d_col, d_val, s))
@@ -394,6 +406,8 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
     // failure here only means the first run loads them)
     if (P.kernel == kKernelSweep) {
         (void)launch_sweep(P, nullptr, nullptr, s, true);
+    } else if (P.kernel == kKernelBinned) {
+        (void)launch_binned(P, nullptr, nullptr, s, true);
     } else if (P.kernel == kKernelBlocked) {
         (void)launch_blocked(P, nullptr, nullptr, s, true);
     } else if (P.kernel == kKernelSlices) {
@@ -508,6 +522,13 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             if (p->locality < 0.3)
                 kernel = kKernelSweep;
         }
+        // fp32, scattered, large: the two-pass binned kernel (binned.hip) streams 16 B per
+        // non-zero instead of gathering x lines. Measured on the power-law generator
+        // (profiles/r02_binned.jsonl): 4M rows / 64M nnz 0.203 vs 0.199 ms (sweep), 6M / 96M
+        // 0.317 vs 0.374, 10M / 160M 0.457 vs 0.616, 20M / 320M 0.964 vs 1.450. In fp64 (28 B
+        // per non-zero) the sweep stays faster at 10M / 160M (0.79 vs 0.82 ms).
+        if (kernel == kKernelSweep && sizeof(ValueType) == 4 && nnz >= 80000000ull && nr_cols >= 5000000u)
+            kernel = kKernelBinned;
     }
     trace("validate + kernel choice", s);
     if (const char *t = std::getenv("SPMV_SWEEP_THREADS")) {
@@ -582,7 +603,8 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     } else {
         if (build_layout(*p, kernel, requested_kernel() < 0, h_row_ptr, d_col, d_val, s))
             return 1;
-        trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel != kKernelTiles ? "build CSR layout"
+        trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelBinned ? "build binned layout"
+              : p->kernel != kKernelTiles ? "build CSR layout"
                                                                                         : "build tile layout", s);
     }
     *out = p.release();
@@ -602,7 +624,8 @@ spmv_plan::~spmv_plan()
                       (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
-                      (void *)d_sbase, (void *)d_slice_len})
+                      (void *)d_sbase, (void *)d_slice_len, (void *)d_b_val, (void *)d_b_colw, (void *)d_b_rowp,
+                      (void *)d_b_prod, (void *)d_b_seg, (void *)d_b_ub, (void *)d_b_uwin})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -624,6 +647,9 @@ uint64_t spmv_plan::device_bytes() const
     if (kernel == kKernelBlocked)  // entries, kptr, kpos, rl, partials, rp2, chunks, units
         return nnz * (2 + sizeof(ValueType)) + (nkpairs + 1) * 4 + nkpairs * (4 + 2 + sizeof(ValueType)) +
                (uint64_t(nr_rows) + 1) * 4 + (nchunks + 1) * 4 + nunits * 8 + 4;
+    if (kernel == kKernelBinned)  // entries (value, 2 offsets), products, segments, units, panels
+        return ent_pad * (2 * sizeof(ValueType) + 4) + (uint64_t(b_nwin) * npanels + 1) * 8 + (b_nunits + 1) * 12 +
+               (npanels + 1) * 4;
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
@@ -713,6 +739,7 @@ static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStrea
     }
     if (p->kernel != kKernelTiles) {
         SPMV_TRY(p->kernel == kKernelSweep     ? launch_sweep(*p, d_x, d_y, s)
+                 : p->kernel == kKernelBinned  ? launch_binned(*p, d_x, d_y, s)
                  : p->kernel == kKernelBlocked ? launch_blocked(*p, d_x, d_y, s)
                  : p->kernel == kKernelSlices  ? launch_slices(*p, d_x, d_y, s)
                                                : launch_gold(*p, d_x, d_y, s));
@@ -804,11 +831,13 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     // work units of the main kernel: tiles, sweep units (panel pieces), or long rows (gold)
     const bool csr = p->kernel == kKernelGold || p->kernel == kKernelFpga;
     st->nr_tiles = (p->kernel == kKernelSweep || p->kernel == kKernelBlocked) ? p->nunits
+                   : p->kernel == kKernelBinned                               ? p->npanels
                    : p->kernel == kKernelSlices                               ? p->nslices
                    : csr                                                      ? p->nlong
                                                                               : p->ntiles;
     st->tile_nnz = p->kernel == kKernelSlices   ? p->slice_slots * kWave  // stored entries with padding
                    : p->kernel == kKernelSweep  ? (p->nunits ? p->ent_pad / p->nunits : 0)
+                   : p->kernel == kKernelBinned ? (p->npanels ? p->ent_pad / p->npanels : 0)
                    : p->kernel == kKernelBlocked ? (p->nunits ? p->nnz / p->nunits : 0)
                    : csr                         ? (uint64_t)kGoldLong
                                                  : kTileNnz;

@@ -51,6 +51,8 @@ constexpr int kKernelFpga = 3;   // the reference FPGA path's order for (VF, blo
 constexpr int kKernelBlocked = 4;  // the same order by the reference's dataflow: x blocks in LDS,
                                    // per-block partials, block-ordered merge (blocked.hip)
 constexpr int kKernelSlices = 5;   // wave per 64 rows, entries slot-major (slices.hip)
+constexpr int kKernelBinned = 6;   // two passes: products per column window, summed per row panel
+                                   // (propagation blocking, binned.hip)
 constexpr int kGoldLong = 128;   // gold plan stats: rows longer than this count as long
 
 }  // namespace spmvhw
@@ -129,6 +131,17 @@ struct spmv_plan {
     bool sweep_packed = false;
     bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)
     bool sweep_det = false;          // env SPMV_SWEEP_DETERMINISTIC=1: ordered LDS adds (k_spmv_sweep_turn)
+    // binned representation (kernel 6, binned.hip): reuses npanels, panel_rmax, d_panel_row and
+    // ent_pad of the sweep fields; entries ordered (window, panel), segments padded
+    uint32_t b_nwin = 0, b_W = 0;      // column windows of b_W columns (x staged in LDS by pass 1)
+    uint64_t b_nunits = 0;             // pass-1 work units
+    ValueType *d_b_val = nullptr;
+    uint16_t *d_b_colw = nullptr;      // column - window base
+    uint16_t *d_b_rowp = nullptr;      // row - panel base (pad entries: the scratch slot)
+    ValueType *d_b_prod = nullptr;     // products, written by pass 1 and read by pass 2
+    uint64_t *d_b_seg = nullptr;       // padded segment offsets [b_nwin * npanels + 1]
+    uint64_t *d_b_ub = nullptr;        // pass-1 unit boundaries [b_nunits + 1]
+    uint32_t *d_b_uwin = nullptr;      // window of each pass-1 unit
     double locality = -1.0;    // probe result used by the automatic kernel choice
     double tuned_ms[3] = {-1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: measured tiles / sweep / slices ms
 
@@ -198,6 +211,12 @@ int build_blocked(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_sr
 // slices.hip
 hipError_t launch_slices(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
 int build_slices(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
+                 hipStream_t s);
+
+// binned.hip
+hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
+// 0 ok, 1 error, 2 the segment table would be too large (caller may use another kernel)
+int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                  hipStream_t s);
 
 // sweep.hip

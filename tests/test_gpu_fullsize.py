@@ -3,7 +3,7 @@ kernel, against the CPU oracle's restatement of spmv_gold (csr.cpp:184-194):
 
   config 2: banded 1,000,000 x 1,000,000, 16 nnz/row, fp64        -> flagged tiles (kernel 0)
   config 3: power-law 10M x 10M, 160M nnz, fp64                   -> panel sweep (kernel 2)
-  config 5: the config-3 matrix in fp32                            -> panel sweep (kernel 2)
+  config 5: the config-3 matrix in fp32                            -> two-pass binned (kernel 6)
 
 Componentwise-scaled error max_i |dy_i| / (|A||x|)_i <= 1e-6 (fp64) / 1e-4 (fp32), the
 north_star tolerance; fp64 is also held to 1e-12. The matrices are the bench's (same generator,
@@ -51,16 +51,30 @@ def test_config2_banded_1m_x16_fp64_auto_tiles():
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("dtype", [np.float64, np.float32], ids=["config3_fp64", "config5_fp32"])
-def test_config3_and_5_powerlaw_10m_160m_auto_sweep(dtype):
+def test_config3_and_5_powerlaw_10m_160m_auto(dtype):
     lib = spmv_hw.load(dtype)
     n, z = 10_000_000, 160_000_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
     x = spmv_hw.gen_vector(lib, n, seed=6)
-    err, st = _run(lib, rp, col, val, x, n, expect_kernel=2)
+    err, st = _run(lib, rp, col, val, x, n, expect_kernel=2 if np.dtype(dtype) == np.float64 else 6)
     assert st["nr_nzeros"] == z and st["nr_rows"] == n
     assert err <= TOL[np.dtype(dtype)], err
     if np.dtype(dtype) == np.float64:
         assert err <= 1e-12, err
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_config3_and_5_binned_forced(monkeypatch, dtype):
+    """The binned kernel (kernel 6) on the headline matrix in both precisions (fp64 forced: the
+    automatic choice keeps the sweep there)."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "binned")
+    lib = spmv_hw.load(dtype)
+    n, z = 10_000_000, 160_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    err, st = _run(lib, rp, col, val, x, n, expect_kernel=6)
+    assert err <= (1e-12 if np.dtype(dtype) == np.float64 else 1e-4), err
 
 
 @pytest.mark.timeout(600)

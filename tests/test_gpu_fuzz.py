@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 SEEDS = list(range(48))
 FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "slices", "slices_wide",
-                "slices_acc32", "fpga", "blocked", "auto", "tune"]
+                "slices_acc32", "fpga", "blocked", "binned", "auto", "tune"]
 ENV = {"tiles_wide": {"SPMV_TILE_NARROW": "0"}, "sweep_unpacked": {"SPMV_SWEEP_PACKED": "0"},
        "sweep_det": {"SPMV_SWEEP_DETERMINISTIC": "1"},
        "slices_wide": {"SPMV_SLICE_NARROW": "0"}, "slices_acc32": {"SPMV_SLICE_ACC": "32"}}
@@ -100,7 +100,7 @@ def test_fuzz(torch, monkeypatch, seed, kern, dtype):
     lib = spmv_hw.load(dtype)
     y, st = run_device(torch, lib, row_ptr, col, val, x, m)
     if kern in ("auto", "tune"):  # the automatic choice / the timed choice among tiles, sweep, slices
-        assert st["kernel"] in (0, 2, 5)
+        assert st["kernel"] in (0, 2, 5, 6)
     else:
         assert st["kernel"] == KERNEL_ID[kern.split("_")[0]]
     if kern == "gold" or (kern.startswith("slices") and (dtype == np.float64 or kern == "slices_acc32")):

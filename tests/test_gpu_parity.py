@@ -28,9 +28,10 @@ def torch():
     return t
 
 
-KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "blocked", "slices", "slices_wide"]
+KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "blocked", "slices", "slices_wide",
+           "binned"]
 KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "sweep_det": 2, "gold": 1, "blocked": 4,
-             "slices": 5, "slices_wide": 5}
+             "slices": 5, "slices_wide": 5, "binned": 6}
 
 
 @pytest.fixture(params=KERNELS)
@@ -41,7 +42,7 @@ def kernel(request, monkeypatch):
     "sweep_unpacked" the sweep on 14-byte entries (SPMV_SWEEP_PACKED=0), the layout used when a
     chunk of a panel spans >= 65536 columns; "sweep_det" the deterministic sweep
     (SPMV_SWEEP_DETERMINISTIC=1); "slices_wide" the slice kernel with 32-bit columns
-    (SPMV_SLICE_NARROW=0)."""
+    (SPMV_SLICE_NARROW=0); "binned" the two-pass propagation-blocking kernel (binned.hip)."""
     monkeypatch.setenv("SPMV_HW_KERNEL", request.param.split("_")[0])
     if request.param == "tiles_wide":
         monkeypatch.setenv("SPMV_TILE_NARROW", "0")
@@ -754,7 +755,7 @@ def test_clustered_tile_columns(torch, monkeypatch, dtype, gaps, clustered):
 def test_auto_kernel_choice(torch, monkeypatch):
     """Automatic choice: banded (local columns, 8-bit spans) -> tiles; 3-D stencils (rows of equal
     length, 16-bit slot spans) -> slices; power-law with columns spread over an x much larger
-    than the L2s -> sweep."""
+    than the L2s -> sweep (fp32 from 80M non-zeros: binned)."""
     monkeypatch.delenv("SPMV_HW_KERNEL", raising=False)
     lib = spmv_hw.load(np.float64)
     n = 6_000_000
@@ -768,6 +769,12 @@ def test_auto_kernel_choice(torch, monkeypatch):
     for n, want in ((300_000, 2), (100_000, 0)):
         rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 16 * n)
         assert spmv_hw.Plan.from_device(lib, rp, col, val, n).stats()["kernel"] == want, n
+    # fp32: the two-pass binned kernel once the matrix is large (>= 80M non-zeros, >= 5M columns)
+    lib32 = spmv_hw.load(np.float32)
+    for n, want in ((6_000_000, 6), (4_000_000, 2)):
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib32, n, n, 16 * n)
+        assert spmv_hw.Plan.from_device(lib32, rp, col, val, n).stats()["kernel"] == want, n
+        del rp, col, val
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     from ab_variants import stencil
     for points in (7, 27):
