@@ -82,7 +82,8 @@ typedef struct spmv_plan_stats {
     uint64_t nr_nzeros;          /* stored non-zeros */
     uint64_t nr_nonempty_rows;   /* rows with >= 1 non-zero */
     uint64_t nr_tiles;           /* work units of the main kernel: wave tiles (0), long rows (1, 3),
-                                    panel pieces (2), phase-1 units (4), 64-row slices (5) */
+                                    panel pieces (2), phase-1 units (4), 64-row slices (5),
+                                    row panels of pass 2 (6) */
     uint64_t tile_nnz;           /* non-zeros per unit (kernel 5: stored entries with padding) */
     uint64_t device_bytes;       /* bytes of the hw representation resident in HBM */
     uint64_t algorithmic_bytes;  /* compulsory CSR bytes per SpMV, SURVEY.md §8(d) */
@@ -92,10 +93,13 @@ typedef struct spmv_plan_stats {
                                     SPMV_FPGA_VF / SPMV_FPGA_BLOCK (bitwise), 4 = the same order
                                     by the reference's column-blocked dataflow (x blocks in LDS),
                                     5 = slices (wave per 64 rows, slot-major; DESIGN.md §3-4;
-                                    fp64: bitwise spmv_gold; fp32 too with env SPMV_SLICE_ACC=32).
-                                    Chosen automatically (0, 2 or 5), or by env SPMV_HW_KERNEL =
-                                    tiles | gold | sweep | fpga | blocked | slices | tune (build
-                                    tiles, sweep and slices, time them on the matrix, keep the
+                                    fp64: bitwise spmv_gold; fp32 too with env SPMV_SLICE_ACC=32),
+                                    6 = binned (two passes: products per column window, summed
+                                    per row panel in LDS; binned.hip).
+                                    Chosen automatically (0, 2, 5, or 6 for large scattered fp32
+                                    matrices), or by env SPMV_HW_KERNEL = tiles | gold | sweep |
+                                    fpga | blocked | slices | binned | tune (build
+                                    tiles, sweep, slices and binned, time them on the matrix, keep the
                                     fastest) */
     int32_t blocks;              /* column blocks of the representation (kernel 4; 1 otherwise) */
     int32_t format;              /* bit 0: 16- or 8-bit column offsets (per tile, kernel 0; per

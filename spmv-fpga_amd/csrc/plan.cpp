@@ -549,30 +549,38 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         return q;
     };
     if (kernel == kKernelTune) {
-        // build the tile, sweep and slice layouts, time one SpMV of each on this matrix, keep
-        // the fastest
-        std::unique_ptr<spmv_plan> q = fresh(), r = fresh();
+        // build the tile, sweep, slice and binned layouts, time one SpMV of each on this matrix,
+        // keep the fastest
+        std::unique_ptr<spmv_plan> q = fresh(), r = fresh(), b = fresh();
         r->slice_pad_limit = 2.0;  // a slice layout padded beyond 2x is built as tiles instead
         if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s) ||
             build_layout(*q, kKernelSweep, true, h_row_ptr, d_col, d_val, s) ||
-            build_layout(*r, kKernelSlices, true, h_row_ptr, d_col, d_val, s))
+            build_layout(*r, kKernelSlices, true, h_row_ptr, d_col, d_val, s) ||
+            build_layout(*b, kKernelBinned, true, h_row_ptr, d_col, d_val, s))
             return 1;
         Tmp tx, ty;
         SPMV_TRY(hipMalloc(&tx.p, std::max<size_t>(nr_cols, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMalloc(&ty.p, std::max<size_t>(nr_rows, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMemsetAsync(tx.p, 0, std::max<size_t>(nr_cols, 1) * sizeof(ValueType), s));
-        double mt = 1e30, ms = 1e30, ml = 1e30;
+        double mt = 1e30, ms = 1e30, ml = 1e30, mb = 1e30;
         if (time_layout(*p, (const ValueType *)tx.p, (ValueType *)ty.p, s, &mt) ||
             time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ms) ||
-            time_layout(*r, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ml))
+            time_layout(*r, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ml) ||
+            time_layout(*b, (const ValueType *)tx.p, (ValueType *)ty.p, s, &mb))
             return 1;
-        if (ms < mt && ms <= ml)
+        const double best = std::min({mt, ms, ml, mb});
+        if (mt == best)
+            ;  // ties keep the tiles
+        else if (ms == best)
             p.swap(q);
-        else if (ml < mt && ml < ms)
+        else if (ml == best)
             p.swap(r);
+        else if (mb == best)
+            p.swap(b);
         p->tuned_ms[0] = mt;
         p->tuned_ms[1] = ms;
         p->tuned_ms[2] = ml;
+        p->tuned_ms[3] = mb;
         trace("tune: build all + time", s);
     } else if (requested_kernel() < 0 && kernel == kKernelTiles && nnz >= 65536) {
         // automatic, local columns: the slice layout when rows of a 64-row slice have about the

@@ -143,7 +143,7 @@ struct spmv_plan {
     uint64_t *d_b_ub = nullptr;        // pass-1 unit boundaries [b_nunits + 1]
     uint32_t *d_b_uwin = nullptr;      // window of each pass-1 unit
     double locality = -1.0;    // probe result used by the automatic kernel choice
-    double tuned_ms[3] = {-1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: measured tiles / sweep / slices ms
+    double tuned_ms[4] = {-1.0, -1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: tiles / sweep / slices / binned ms
 
     // timing (HIP events around the main kernel, on the launch stream)
     bool timing = false;

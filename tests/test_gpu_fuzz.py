@@ -99,7 +99,7 @@ def test_fuzz(torch, monkeypatch, seed, kern, dtype):
     monkeypatch.setenv("SPMV_FPGA_BLOCK", str(block))
     lib = spmv_hw.load(dtype)
     y, st = run_device(torch, lib, row_ptr, col, val, x, m)
-    if kern in ("auto", "tune"):  # the automatic choice / the timed choice among tiles, sweep, slices
+    if kern in ("auto", "tune"):  # the automatic choice / the timed choice among tiles, sweep, slices, binned
         assert st["kernel"] in (0, 2, 5, 6)
     else:
         assert st["kernel"] == KERNEL_ID[kern.split("_")[0]]
