@@ -65,7 +65,7 @@ __global__ void k_initx(uint32_t n, V *x)
 }
 
 // pass 1: blockIdx.x = window; entries [w EW, (w+1) EW), EW a multiple of PER
-template <typename V, int U>
+template <typename V, int U, int G = 1, bool NTS = true>
 __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t ncols, uint32_t W, uint64_t EW,
                                               const uint16_t *__restrict__ colw, const V *__restrict__ val,
                                               V *__restrict__ prod)
@@ -103,27 +103,36 @@ __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t 
     __syncthreads();
     const uint64_t e0 = (uint64_t)blockIdx.x * EW, e1 = e0 + EW;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr uint64_t STEP = 64 * PER;
+    constexpr uint64_t STEP = 64 * PER * G;
     for (uint64_t s = e0 + wv * STEP * U; s < e1; s += 16 * STEP * U) {
-        VT v[U];
-        IT c[U];
+        VT v[U][G];
+        IT c[U][G];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t i = s + u * STEP + lane * PER;
+            const uint64_t i = s + u * STEP + lane * PER * G;
             if (i < e1) {
-                v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + i));
-                c[u] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(colw + i));
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    v[u][g] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + i + g * PER));
+                    c[u][g] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(colw + i + g * PER));
+                }
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t i = s + u * STEP + lane * PER;
+            const uint64_t i = s + u * STEP + lane * PER * G;
             if (i < e1) {
-                VT p;
 #pragma unroll
-                for (int k = 0; k < PER; ++k)
-                    p[k] = v[u][k] * xs[c[u][k]];
-                __builtin_nontemporal_store(p, reinterpret_cast<VT *>(prod + i));
+                for (int g = 0; g < G; ++g) {
+                    VT p;
+#pragma unroll
+                    for (int k = 0; k < PER; ++k)
+                        p[k] = v[u][g][k] * xs[c[u][g][k]];
+                    if (NTS)
+                        __builtin_nontemporal_store(p, reinterpret_cast<VT *>(prod + i + g * PER));
+                    else
+                        *reinterpret_cast<VT *>(prod + i + g * PER) = p;
+                }
             }
         }
     }
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t 
 // pass 2: blockIdx.x = panel; segment (w, p) = entries [(w P + p) L, +L), L a multiple of PER.
 // Wave v takes windows v, v + 16, ...; its segments form one stream of 64 PER-entry steps (the last
 // step of a segment masked), D steps of loads in flight before the adds.
-template <typename V, int D>
+template <typename V, int D, int G = 1>
 __global__ __launch_bounds__(1024) void k_acc(const V *__restrict__ prod, const uint16_t *__restrict__ rowp,
                                               uint32_t nwin, uint32_t npan, uint32_t L, uint32_t R, uint32_t nrows,
                                               V *__restrict__ y)
@@ -148,12 +157,12 @@ __global__ __launch_bounds__(1024) void k_acc(const V *__restrict__ prod, const 
     const uint32_t p = blockIdx.x;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr uint32_t STEP = 64 * PER;
+    constexpr uint32_t STEP = 64 * PER * G;
     uint32_t w = wv;
     uint64_t pos = ((uint64_t)w * npan + p) * L, end = pos + L;
     while (w < nwin) {
-        VT v[D];
-        IT r[D];
+        VT v[D][G];
+        IT r[D][G];
         uint64_t at[D], en[D];
 #pragma unroll
         for (int u = 0; u < D; ++u) {
@@ -162,11 +171,14 @@ __global__ __launch_bounds__(1024) void k_acc(const V *__restrict__ prod, const 
                 pos = ((uint64_t)w * npan + p) * L;
                 end = w < nwin ? pos + L : pos;
             }
-            at[u] = pos + lane * PER;
+            at[u] = pos + lane * PER * G;
             en[u] = end;
             if (at[u] < end) {
-                v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + at[u]));
-                r[u] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(rowp + at[u]));
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    v[u][g] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + at[u] + g * PER));
+                    r[u][g] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(rowp + at[u] + g * PER));
+                }
             }
             pos += STEP;
         }
@@ -174,8 +186,10 @@ __global__ __launch_bounds__(1024) void k_acc(const V *__restrict__ prod, const 
         for (int u = 0; u < D; ++u) {
             if (at[u] < en[u]) {
 #pragma unroll
-                for (int q = 0; q < PER; ++q)
-                    atomicAdd(&ys[r[u][q]], (double)v[u][q]);
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int q = 0; q < PER; ++q)
+                        atomicAdd(&ys[r[u][g][q]], (double)v[u][g][q]);
             }
         }
         if (pos >= end) {
@@ -191,13 +205,13 @@ __global__ __launch_bounds__(1024) void k_acc(const V *__restrict__ prod, const 
             y[r0 + i] = (V)ys[i];
 }
 
-template <typename V, int U, int D>
+template <typename V, int U, int D, int G1 = 1, int G2 = 1, bool NTS = true>
 static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint32_t L, bool check)
 {
     constexpr int PER = 16 / sizeof(V);
     const uint32_t W = ((n + nwin - 1) / nwin + PER - 1) / PER * PER, R = (n + npan - 1) / npan;
     const uint64_t EW = (uint64_t)npan * L, nnz = EW * nwin;
-    if (L % PER || W * sizeof(V) > 160 * 1024 || R * 8 > 160 * 1024 || W > 65536 || R > 65536) {
+    if (L % (PER * G2) || (uint64_t(npan) * L) % (PER * G1) || W * sizeof(V) > 160 * 1024 || R * 8 > 160 * 1024 || W > 65536 || R > 65536) {
         std::fprintf(stderr, "bad shape\n");
         std::exit(1);
     }
@@ -213,8 +227,8 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
     hipLaunchKernelGGL(k_initx<V>, dim3(4096), dim3(256), 0, 0, n, x);
     CHECK(hipDeviceSynchronize());
     const size_t lds1 = W * sizeof(V), lds2 = R * 8;
-    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mul<V, U>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_acc<V, D>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mul<V, U, G1, NTS>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_acc<V, D, G2>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     hipEvent_t ev[3];
     for (auto &evt : ev)
         CHECK(hipEventCreate(&evt));
@@ -222,9 +236,9 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
     const int reps = check ? 1 : 10, warm = check ? 0 : 2;
     for (int it = 0; it < warm + reps; ++it) {
         CHECK(hipEventRecord(ev[0], 0));
-        hipLaunchKernelGGL((k_mul<V, U>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
+        hipLaunchKernelGGL((k_mul<V, U, G1, NTS>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
         CHECK(hipEventRecord(ev[1], 0));
-        hipLaunchKernelGGL((k_acc<V, D>), dim3(npan), dim3(1024), lds2, 0, prod, rowp, nwin, npan, L, R, n, y);
+        hipLaunchKernelGGL((k_acc<V, D, G2>), dim3(npan), dim3(1024), lds2, 0, prod, rowp, nwin, npan, L, R, n, y);
         CHECK(hipEventRecord(ev[2], 0));
         CHECK(hipEventSynchronize(ev[2]));
         float a, b;
@@ -263,9 +277,9 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
                 maxerr = std::fmax(maxerr, std::fabs(ref[r] - (double)hy[r]) / mag[r]);
     }
     std::printf("{\"test\": \"%s\", \"n\": %u, \"nnz\": %llu, \"windows\": %u, \"W\": %u, \"panels\": %u, \"R\": %u, "
-                "\"seg\": %u, \"U\": %d, \"D\": %d, \"pass1_ms\": %.4f, \"pass2_ms\": %.4f, \"total_ms\": %.4f, \"total_ms_160M\": %.4f, "
+                "\"seg\": %u, \"U\": %d, \"D\": %d, \"G1\": %d, \"G2\": %d, \"nts\": %d, \"pass1_ms\": %.4f, \"pass2_ms\": %.4f, \"total_ms\": %.4f, \"total_ms_160M\": %.4f, "
                 "\"pass1_TBps\": %.2f, \"pass2_TBps\": %.2f, \"max_scaled_err\": %.3g}\n",
-                name, n, (unsigned long long)nnz, nwin, W, npan, R, L, U, D, t1, t2, t1 + t2, (t1 + t2) * 160e6 / nnz,
+                name, n, (unsigned long long)nnz, nwin, W, npan, R, L, U, D, G1, G2, (int)NTS, t1, t2, t1 + t2, (t1 + t2) * 160e6 / nnz,
                 b1 / t1 / 1e9, b2 / t2 / 1e9, maxerr);
     std::fflush(stdout);
     CHECK(hipFree(colw));
@@ -280,23 +294,25 @@ int main(int argc, char **argv)
 {
     const bool check = argc > 1 && !std::strcmp(argv[1], "check");
     if (check) {
-        run<float, 4, 4>("check_f32", 200000, 6, 12, 1220, true);
-        run<double, 4, 4>("check_f64", 200000, 12, 12, 610, true);
-        run<float, 8, 8>("check_f32", 200000, 6, 12, 1220, true);
-        run<double, 8, 8>("check_f64", 200000, 12, 12, 610, true);
+        run<float, 4, 8>("check_f32", 200000, 6, 12, 1224, true);
+        run<double, 4, 8>("check_f64", 200000, 12, 12, 612, true);
+        run<float, 4, 8, 2, 2>("check_f32", 200000, 6, 12, 1224, true);
+        run<double, 4, 8, 2, 2, false>("check_f64", 200000, 12, 12, 612, true);
         return 0;
     }
     const uint32_t n = 10000000;
     // fp32: 256 windows of 39,064 columns (156 KiB of x), 512 panels of 19,532 rows
-    run<float, 4, 4>("binned_f32", n, 256, 512, 1220, false);
-    run<float, 8, 4>("binned_f32", n, 256, 512, 1220, false);
-    run<float, 4, 8>("binned_f32", n, 256, 512, 1220, false);
-    run<float, 8, 8>("binned_f32", n, 256, 512, 1220, false);
-    run<float, 4, 8>("binned_f32_p1024", n, 256, 1024, 612, false);
+    run<float, 4, 8>("binned_f32", n, 256, 512, 1224, false);
+    run<float, 4, 8, 2, 2>("binned_f32", n, 256, 512, 1224, false);
+    run<float, 2, 4, 2, 2>("binned_f32", n, 256, 512, 1224, false);
+    run<float, 4, 8, 1, 1, false>("binned_f32", n, 256, 512, 1224, false);
+    run<float, 4, 8, 2, 2, false>("binned_f32", n, 256, 512, 1224, false);
     // fp64: 512 windows of 19,532 columns, 512 panels
-    run<double, 4, 4>("binned_f64", n, 512, 512, 610, false);
-    run<double, 8, 8>("binned_f64", n, 512, 512, 610, false);
-    run<double, 4, 8>("binned_f64", n, 512, 512, 610, false);
-    run<double, 4, 8>("binned_f64_p1024", n, 512, 1024, 306, false);
+    run<double, 4, 8>("binned_f64", n, 512, 512, 612, false);
+    run<double, 4, 8, 2, 2>("binned_f64", n, 512, 512, 612, false);
+    run<double, 2, 4, 2, 2>("binned_f64", n, 512, 512, 612, false);
+    run<double, 4, 8, 1, 1, false>("binned_f64", n, 512, 512, 612, false);
+    run<double, 4, 8, 2, 2, false>("binned_f64", n, 512, 512, 612, false);
+    run<double, 4, 4, 2, 4>("binned_f64", n, 512, 512, 616, false);
     return 0;
 }
