@@ -341,6 +341,13 @@ def side_config(args, name, dev, stream):
                         "frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                         "alg_bytes_per_launch": alg},
            "parity": {"max_scaled_err": err, "tol": tol, "pass": bool(err <= tol)}}
+    if st["kernel"] == 6 and name == "config5":
+        # PMC traffic of the two binned passes on this matrix (profiles/r02_binned_pmc.json)
+        try:
+            pmc = json.load(open(os.path.join(ROOT, "profiles", "r02_binned_pmc.json")))
+            res["roofline"]["traffic"] = pmc["f32"]["hbm_bytes_per_spmv"]
+        except Exception:
+            res["roofline"]["traffic"] = None
     plan.destroy()
     del rp, col, val, x, y
     torch.cuda.empty_cache()
