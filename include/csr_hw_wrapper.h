@@ -118,7 +118,10 @@ int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *matrix
                           IndexType row_begin, IndexType row_end);
 /* d_y[0:nr_rows) = A * d_x  (overwrite; empty rows get 0). Asynchronous on `stream`. Enqueues
  * only kernels and memsets (when timing is off), so callers may capture it into their own
- * hipGraph, e.g. an iterative solver's SpMV + update + RCCL all-gather step. */
+ * hipGraph, e.g. an iterative solver's SpMV + update + RCCL all-gather step.
+ * The split sweep's partial sums and the binned kernel's products live in plan-owned scratch:
+ * runs of ONE plan must be ordered (same stream, or events between streams); distinct plans
+ * may run concurrently. */
 int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, void *stream);
 /* Iterative / persistent mode: `iters` consecutive SpMVs d_y = A * d_x, captured once into a
  * hipGraph (re-captured when d_x, d_y or iters change) and replayed on `stream` per call, so
