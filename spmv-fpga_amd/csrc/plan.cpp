@@ -529,7 +529,11 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         // 1.450; row slices of the 10M x 10M matrix (x stays 40 MB): 5M rows / 80M nnz 0.251
         // vs 0.312, 2.5M / 40M 0.144 vs 0.178, 1.25M / 20M 0.093 vs 0.106. In fp64 (28 B per
         // non-zero) the sweep stays as fast or faster (10M: 0.79-0.82 vs 0.79; slices slower).
-        if (kernel == kKernelSweep && sizeof(ValueType) == 4 && nr_cols >= 5000000u && nnz >= 16000000ull)
+        // Its pass 2 adds in timing order; SPMV_SWEEP_DETERMINISTIC=1 asks for fixed bits, which
+        // the turn-ordered sweep gives, so the switch keeps the sweep.
+        const char *det = std::getenv("SPMV_SWEEP_DETERMINISTIC");
+        if (kernel == kKernelSweep && sizeof(ValueType) == 4 && nr_cols >= 5000000u && nnz >= 16000000ull &&
+            !(det && det[0] == '1'))
             kernel = kKernelBinned;
     }
     trace("validate + kernel choice", s);

@@ -774,6 +774,10 @@ def test_auto_kernel_choice(torch, monkeypatch):
     for n, want in ((6_000_000, 6), (4_000_000, 2)):
         rp, col, val, _ = spmv_hw.gen_powerlaw(lib32, n, n, 16 * n)
         assert spmv_hw.Plan.from_device(lib32, rp, col, val, n).stats()["kernel"] == want, n
+        if want == 6:  # fixed bits requested: the turn-ordered sweep, not the binned kernel
+            monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
+            assert spmv_hw.Plan.from_device(lib32, rp, col, val, n).stats()["kernel"] == 2
+            monkeypatch.delenv("SPMV_SWEEP_DETERMINISTIC")
         del rp, col, val
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     from ab_variants import stencil
