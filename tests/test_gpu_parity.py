@@ -264,6 +264,25 @@ def test_nan_in_unused_x_does_not_leak(torch, kernel):
     assert not np.any(np.isnan(y))
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_unaligned_x_and_y(torch, kernel, dtype):
+    """x and y given as views one element into their buffers (not 16-byte aligned): kernels
+    that stage x with 16-byte loads (the binned kernel's pass 1) take their element-wise path."""
+    rng = np.random.default_rng(17)
+    n, m = 20_000, 70_000
+    row_ptr, col, val, x = random_csr(rng, n, m, rng.integers(0, 40, n), dtype)
+    lib = spmv_hw.load(dtype)
+    plan = spmv_hw.Plan.from_device(lib, to_dev(torch, row_ptr), to_dev(torch, col), to_dev(torch, val), m)
+    xb = to_dev(torch, np.concatenate([np.zeros(1, dtype), x]))
+    yb = torch.full((n + 1,), float("nan"), dtype=xb.dtype, device="cuda")
+    plan.run(xb[1:], yb[1:])
+    torch.cuda.synchronize()
+    plan.destroy()
+    y = yb.cpu().numpy()
+    assert np.isnan(y[0]), "wrote before y"
+    check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y[1:], dtype)
+
+
 def test_out_of_range_column_is_rejected(torch, kernel):
     lib = spmv_hw.load(np.float64)
     row_ptr = np.array([0, 2], np.uint32)
