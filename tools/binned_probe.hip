@@ -205,7 +205,156 @@ __global__ __launch_bounds__(1024) void k_acc(const V *__restrict__ prod, const 
             y[r0 + i] = (V)ys[i];
 }
 
-template <typename V, int U, int D, int G1 = 1, int G2 = 1, bool NTS = true>
+// Software-pipelined forms: the loads of the next batch are issued before the current batch's
+// products (pass 1) or adds (pass 2); pass 1 also issues its first batch before the x window is
+// written to LDS.
+template <typename V, int U>
+__global__ __launch_bounds__(1024) void k_mul_pipe(const V *__restrict__ x, uint32_t ncols, uint32_t W, uint64_t EW,
+                                                   const uint16_t *__restrict__ colw, const V *__restrict__ val,
+                                                   V *__restrict__ prod)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    V *xs = reinterpret_cast<V *>(smem);
+    typedef typename Vec<V>::T VT;
+    typedef typename Vec<V>::I IT;
+    constexpr int PER = 16 / sizeof(V);
+    constexpr uint64_t STEP = 64 * PER;
+    constexpr uint64_t STRIDE = 16 * STEP * U;
+    struct Batch { VT v[U]; IT c[U]; };
+    const uint64_t e0 = (uint64_t)blockIdx.x * EW, e1 = e0 + EW;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    auto load = [&](uint64_t s, Batch &b) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint64_t i = s + k * STEP + lane * PER;
+            if (i < e1) {
+                b.v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + i));
+                b.c[k] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(colw + i));
+            }
+        }
+    };
+    auto comp = [&](uint64_t s, const Batch &b) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint64_t i = s + k * STEP + lane * PER;
+            if (i < e1) {
+                VT pr;
+#pragma unroll
+                for (int q = 0; q < PER; ++q)
+                    pr[q] = b.v[k][q] * xs[b.c[k][q]];
+                __builtin_nontemporal_store(pr, reinterpret_cast<VT *>(prod + i));
+            }
+        }
+    };
+    const uint64_t c0 = (uint64_t)blockIdx.x * W;
+    VT t[10];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t i = (r * 1024 + threadIdx.x) * PER;
+        if (i < W) {
+            if (c0 + i + PER <= ncols) {
+                t[r] = *reinterpret_cast<const VT *>(x + c0 + i);
+            } else {
+#pragma unroll
+                for (int q = 0; q < PER; ++q)
+                    t[r][q] = c0 + i + q < ncols ? x[c0 + i + q] : V(0);
+            }
+        }
+    }
+    uint64_t s = e0 + wv * STEP * U;
+    Batch A, B;
+    if (s < e1)
+        load(s, A);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t i = (r * 1024 + threadIdx.x) * PER;
+        if (i < W)
+            *reinterpret_cast<VT *>(xs + i) = t[r];
+    }
+    __syncthreads();
+    while (s < e1) {
+        uint64_t s2 = s + STRIDE;
+        if (s2 < e1)
+            load(s2, B);
+        comp(s, A);
+        s = s2;
+        if (s >= e1)
+            break;
+        s2 = s + STRIDE;
+        if (s2 < e1)
+            load(s2, A);
+        comp(s, B);
+        s = s2;
+    }
+}
+
+template <typename V, int D>
+__global__ __launch_bounds__(1024) void k_acc_pipe(const V *__restrict__ prod, const uint16_t *__restrict__ rowp,
+                                                   uint32_t nwin, uint32_t npan, uint32_t L, uint32_t R,
+                                                   uint32_t nrows, V *__restrict__ y)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double *ys = reinterpret_cast<double *>(smem);
+    typedef typename Vec<V>::T VT;
+    typedef typename Vec<V>::I IT;
+    constexpr int PER = 16 / sizeof(V);
+    constexpr uint32_t STEP = 64 * PER;
+    struct Batch { VT v[D]; IT r[D]; uint64_t at[D], en[D]; };
+    for (uint32_t i = threadIdx.x; i < R; i += 1024)
+        ys[i] = 0.0;
+    __syncthreads();
+    const uint32_t p = blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t w = wv;
+    uint64_t pos = ((uint64_t)w * npan + p) * L, end = w < nwin ? pos + L : pos;
+    auto load = [&](Batch &b) -> bool {
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+            while (pos >= end && w < nwin) {
+                w += 16;
+                pos = ((uint64_t)w * npan + p) * L;
+                end = w < nwin ? pos + L : pos;
+            }
+            any |= w < nwin;
+            b.at[u] = pos + lane * PER;
+            b.en[u] = w < nwin ? end : 0;
+            if (b.at[u] < b.en[u]) {
+                b.v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + b.at[u]));
+                b.r[u] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(rowp + b.at[u]));
+            }
+            pos += STEP;
+        }
+        return any;
+    };
+    auto add = [&](const Batch &b) {
+#pragma unroll
+        for (int u = 0; u < D; ++u)
+            if (b.at[u] < b.en[u]) {
+#pragma unroll
+                for (int q = 0; q < PER; ++q)
+                    atomicAdd(&ys[b.r[u][q]], (double)b.v[u][q]);
+            }
+    };
+    Batch A, B;
+    bool ha = load(A);
+    while (ha) {
+        const bool hb = load(B);
+        add(A);
+        if (!hb)
+            break;
+        ha = load(A);
+        add(B);
+    }
+    __syncthreads();
+    const uint64_t r0 = (uint64_t)p * R;
+    for (uint32_t i = threadIdx.x; i < R; i += 1024)
+        if (r0 + i < nrows)
+            y[r0 + i] = (V)ys[i];
+}
+
+template <typename V, int U, int D, int G1 = 1, int G2 = 1, bool NTS = true, bool PIPE = false>
 static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint32_t L, bool check)
 {
     constexpr int PER = 16 / sizeof(V);
@@ -228,6 +377,8 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
     CHECK(hipDeviceSynchronize());
     const size_t lds1 = W * sizeof(V), lds2 = R * 8;
     CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mul<V, U, G1, NTS>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mul_pipe<V, U>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_acc_pipe<V, D>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_acc<V, D, G2>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     hipEvent_t ev[3];
     for (auto &evt : ev)
@@ -236,9 +387,15 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
     const int reps = check ? 1 : 10, warm = check ? 0 : 2;
     for (int it = 0; it < warm + reps; ++it) {
         CHECK(hipEventRecord(ev[0], 0));
-        hipLaunchKernelGGL((k_mul<V, U, G1, NTS>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
+        if (PIPE)
+            hipLaunchKernelGGL((k_mul_pipe<V, U>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
+        else
+            hipLaunchKernelGGL((k_mul<V, U, G1, NTS>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
         CHECK(hipEventRecord(ev[1], 0));
-        hipLaunchKernelGGL((k_acc<V, D, G2>), dim3(npan), dim3(1024), lds2, 0, prod, rowp, nwin, npan, L, R, n, y);
+        if (PIPE)
+            hipLaunchKernelGGL((k_acc_pipe<V, D>), dim3(npan), dim3(1024), lds2, 0, prod, rowp, nwin, npan, L, R, n, y);
+        else
+            hipLaunchKernelGGL((k_acc<V, D, G2>), dim3(npan), dim3(1024), lds2, 0, prod, rowp, nwin, npan, L, R, n, y);
         CHECK(hipEventRecord(ev[2], 0));
         CHECK(hipEventSynchronize(ev[2]));
         float a, b;
@@ -279,7 +436,7 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
     std::printf("{\"test\": \"%s\", \"n\": %u, \"nnz\": %llu, \"windows\": %u, \"W\": %u, \"panels\": %u, \"R\": %u, "
                 "\"seg\": %u, \"U\": %d, \"D\": %d, \"G1\": %d, \"G2\": %d, \"nts\": %d, \"pass1_ms\": %.4f, \"pass2_ms\": %.4f, \"total_ms\": %.4f, \"total_ms_160M\": %.4f, "
                 "\"pass1_TBps\": %.2f, \"pass2_TBps\": %.2f, \"max_scaled_err\": %.3g}\n",
-                name, n, (unsigned long long)nnz, nwin, W, npan, R, L, U, D, G1, G2, (int)NTS, t1, t2, t1 + t2, (t1 + t2) * 160e6 / nnz,
+                name, n, (unsigned long long)nnz, nwin, W, npan, R, L, U, D, G1, G2, (int)NTS, (int)PIPE, t1, t2, t1 + t2, (t1 + t2) * 160e6 / nnz,
                 b1 / t1 / 1e9, b2 / t2 / 1e9, maxerr);
     std::fflush(stdout);
     CHECK(hipFree(colw));
@@ -294,25 +451,21 @@ int main(int argc, char **argv)
 {
     const bool check = argc > 1 && !std::strcmp(argv[1], "check");
     if (check) {
-        run<float, 4, 8>("check_f32", 200000, 6, 12, 1224, true);
-        run<double, 4, 8>("check_f64", 200000, 12, 12, 612, true);
-        run<float, 4, 8, 2, 2>("check_f32", 200000, 6, 12, 1224, true);
-        run<double, 4, 8, 2, 2, false>("check_f64", 200000, 12, 12, 612, true);
+        run<float, 4, 8, 1, 1, true, true>("check_f32_pipe", 200000, 6, 12, 1224, true);
+        run<double, 4, 8, 1, 1, true, true>("check_f64_pipe", 200000, 12, 12, 612, true);
+        run<float, 4, 4, 1, 1, true, true>("check_f32_pipe", 200000, 6, 12, 1224, true);
         return 0;
     }
     const uint32_t n = 10000000;
-    // fp32: 256 windows of 39,064 columns (156 KiB of x), 512 panels of 19,532 rows
-    run<float, 4, 8>("binned_f32", n, 256, 512, 1224, false);
-    run<float, 4, 8, 2, 2>("binned_f32", n, 256, 512, 1224, false);
-    run<float, 2, 4, 2, 2>("binned_f32", n, 256, 512, 1224, false);
-    run<float, 4, 8, 1, 1, false>("binned_f32", n, 256, 512, 1224, false);
-    run<float, 4, 8, 2, 2, false>("binned_f32", n, 256, 512, 1224, false);
-    // fp64: 512 windows of 19,532 columns, 512 panels
-    run<double, 4, 8>("binned_f64", n, 512, 512, 612, false);
-    run<double, 4, 8, 2, 2>("binned_f64", n, 512, 512, 612, false);
-    run<double, 2, 4, 2, 2>("binned_f64", n, 512, 512, 612, false);
-    run<double, 4, 8, 1, 1, false>("binned_f64", n, 512, 512, 612, false);
-    run<double, 4, 8, 2, 2, false>("binned_f64", n, 512, 512, 612, false);
-    run<double, 4, 4, 2, 4>("binned_f64", n, 512, 512, 616, false);
+    for (int rep = 0; rep < 2; ++rep) {
+        run<float, 4, 8>("binned_f32", n, 256, 512, 1224, false);
+        run<float, 4, 8, 1, 1, true, true>("binned_f32_pipe", n, 256, 512, 1224, false);
+        run<float, 4, 4, 1, 1, true, true>("binned_f32_pipe", n, 256, 512, 1224, false);
+        run<float, 2, 4, 1, 1, true, true>("binned_f32_pipe", n, 256, 512, 1224, false);
+        run<double, 4, 8>("binned_f64", n, 512, 512, 612, false);
+        run<double, 4, 8, 1, 1, true, true>("binned_f64_pipe", n, 512, 512, 612, false);
+        run<double, 4, 4, 1, 1, true, true>("binned_f64_pipe", n, 512, 512, 612, false);
+        run<double, 2, 4, 1, 1, true, true>("binned_f64_pipe", n, 512, 512, 612, false);
+    }
     return 0;
 }
