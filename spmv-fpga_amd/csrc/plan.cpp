@@ -615,6 +615,8 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             trace("build tile layout", s);
         }
     } else {
+        if (kernel == kKernelBinned && requested_kernel() < 0)
+            p->bin_skew_limit = 2.0;  // automatic: skewed matrices stay on the sweep
         if (build_layout(*p, kernel, requested_kernel() < 0, h_row_ptr, d_col, d_val, s))
             return 1;
         trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelBinned ? "build binned layout"

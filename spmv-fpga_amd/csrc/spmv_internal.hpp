@@ -142,6 +142,9 @@ struct spmv_plan {
     uint64_t *d_b_seg = nullptr;       // padded segment offsets [b_nwin * npanels + 1]
     uint64_t *d_b_ub = nullptr;        // pass-1 unit boundaries [b_nunits + 1]
     uint32_t *d_b_uwin = nullptr;      // window of each pass-1 unit
+    double bin_skew_limit = 0.0;       // automatic choice: give up (rc 2) when a panel holds more than
+                                       // this many times the mean entries (long rows: pass 2 would
+                                       // serialise their LDS adds on one address)
     double locality = -1.0;    // probe result used by the automatic kernel choice
     double tuned_ms[4] = {-1.0, -1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: tiles / sweep / slices / binned ms
 

@@ -805,6 +805,39 @@ def test_auto_kernel_choice(torch, monkeypatch):
         assert spmv_hw.Plan.from_device(lib, rp, col, val, n).stats()["kernel"] == 5, points
 
 
+def test_auto_binned_skips_skewed_fp32(torch, monkeypatch):
+    """fp32 with x of 6M columns would take the binned kernel, but one row of 2M entries makes
+    its panel 2x+ the mean: pass 2 would serialise that row's LDS adds on one address (2.6 vs
+    0.42 ms, tools/skew_probe.py), so the automatic choice keeps the sweep, which cuts such
+    panels into pieces. Forced, the binned kernel still gives the right y."""
+    monkeypatch.delenv("SPMV_HW_KERNEL", raising=False)
+    lib = spmv_hw.load(np.float32)
+    n, m, z, dense = 1_200_000, 6_000_000, 19_200_000, 2_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, z, seed=9)
+    dcol = torch.arange(0, 3 * dense, 3, dtype=torch.int32, device="cuda")
+    rp = torch.cat([rp, (rp[-1:].long() + dense).int()])
+    col = torch.cat([col[:z], dcol])
+    val = torch.cat([val[:z], torch.full((dense,), 0.5, dtype=val.dtype, device="cuda")])
+    x = spmv_hw.gen_vector(lib, m, seed=6)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref = oracle.spmv_gold(row_ptr, c, v, xx)
+    for forced, want in ((None, 2), ("binned", 6)):
+        if forced:
+            monkeypatch.setenv("SPMV_HW_KERNEL", forced)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, m)
+        assert plan.stats()["kernel"] == want
+        y = torch.full((n + 1,), float("nan"), dtype=x.dtype, device="cuda")
+        plan.run(x, y)
+        torch.cuda.synchronize()
+        plan.destroy()
+        # against spmv_gold's own fp32 running sum over the 2M-entry row: the north_star
+        # tolerance (the fp64-accumulating kernels are the more accurate side here)
+        yy = y.cpu().numpy()
+        assert not np.isnan(yy).any()
+        assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TOL[np.dtype(np.float32)]
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("points", [7, 27])
 def test_slices_stencil_narrow_equals_wide(torch, monkeypatch, dtype, points):

@@ -24,7 +24,10 @@ def main():
     ap.add_argument("--dense", type=int, default=2_000_000)
     ap.add_argument("--ndense", type=int, default=2)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--dtype", default="f64")
+    ap.add_argument("--kernels", default="tiles,sweep,gold")
     a = ap.parse_args()
+    dtype = np.float64 if a.dtype == "f64" else np.float32
     rng = np.random.default_rng(5)
     n, m = a.rows, a.cols
     lens = rng.poisson(16, n).astype(np.int64)
@@ -45,18 +48,18 @@ def main():
             while len(c) < k:
                 c = np.unique(np.concatenate([c, rng.integers(0, m, k - len(c))]))
         col[rp[r]:rp[r + 1]] = c
-    val = rng.uniform(-1, 1, z)
-    x = rng.uniform(0, 1, m)
+    val = rng.uniform(-1, 1, z).astype(dtype)
+    x = rng.uniform(0, 1, m).astype(dtype)
     rp = rp.astype(np.uint32)
     ref = oracle.spmv_gold(rp, col, val, x)
-    lib = spmv_hw.load(np.float64)
+    lib = spmv_hw.load(dtype)
     d = lambda t: torch.from_numpy(t.view(np.int32) if t.dtype == np.uint32 else t).cuda()
     drp, dcol, dval, dx = d(rp), d(col), d(val), d(x)
-    out = {"rows": n, "cols": m, "nnz": z, "dense_rows": a.ndense, "dense_len": a.dense}
-    for kern in ("tiles", "sweep", "gold"):
-        os.environ["SPMV_HW_KERNEL"] = kern
+    out = {"rows": n, "cols": m, "nnz": z, "dense_rows": a.ndense, "dense_len": a.dense, "dtype": a.dtype}
+    for kern in a.kernels.split(","):
+        os.environ["SPMV_HW_KERNEL"] = kern  # "auto": the automatic choice
         plan = spmv_hw.Plan.from_device(lib, drp, dcol, dval, m)
-        y = torch.empty(n, dtype=torch.float64, device="cuda")
+        y = torch.empty(n, dtype=dx.dtype, device="cuda")
         plan.run(dx, y)
         torch.cuda.synchronize()
         err = oracle.scaled_error(rp, col, val, x, ref, y.cpu().numpy())
@@ -65,7 +68,7 @@ def main():
             plan.run(dx, y)
         ms, _, _ = plan.timing()
         st = plan.stats()
-        out[kern] = {"ms": round(ms, 4), "scaled_err": err, "units": st["nr_tiles"]}
+        out[kern] = {"ms": round(ms, 4), "scaled_err": err, "units": st["nr_tiles"], "kernel": st["kernel"]}
         plan.destroy()
     os.environ.pop("SPMV_HW_KERNEL", None)
     print(json.dumps(out), flush=True)
