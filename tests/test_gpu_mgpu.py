@@ -30,7 +30,10 @@ def _powerlaw_host(lib, n, z):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("exchange", [spmv_hw.MGPU_GATHER, spmv_hw.MGPU_REDUCE])
-def test_mgpu_gather_and_reduce_match_oracle(dtype, exchange):
+@pytest.mark.parametrize("kern", ["auto", "binned"])
+def test_mgpu_gather_and_reduce_match_oracle(monkeypatch, dtype, exchange, kern):
+    if kern != "auto":  # every device's plan on that kernel
+        monkeypatch.setenv("SPMV_HW_KERNEL", kern)
     lib = spmv_hw.load(dtype)
     n, z = 300_000, 4_800_000
     rp, col, val, x = _powerlaw_host(lib, n, z)
