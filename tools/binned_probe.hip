@@ -65,7 +65,9 @@ __global__ void k_initx(uint32_t n, V *x)
 }
 
 // pass 1: blockIdx.x = window; entries [w EW, (w+1) EW), EW a multiple of PER
-template <typename V, int U, int G = 1, bool NTS = true>
+// ABL (measurement only, wrong products): 1 no LDS read (product = value * column offset), 2 no
+// product stores (one sink store per lane), 3 no entry loads (stores of a lane-dependent constant)
+template <typename V, int U, int G = 1, bool NTS = true, int ABL = 0>
 __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t ncols, uint32_t W, uint64_t EW,
                                               const uint16_t *__restrict__ colw, const V *__restrict__ val,
                                               V *__restrict__ prod)
@@ -104,6 +106,7 @@ __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t 
     const uint64_t e0 = (uint64_t)blockIdx.x * EW, e1 = e0 + EW;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     constexpr uint64_t STEP = 64 * PER * G;
+    VT sink = {};
     for (uint64_t s = e0 + wv * STEP * U; s < e1; s += 16 * STEP * U) {
         VT v[U][G];
         IT c[U][G];
@@ -113,8 +116,13 @@ __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t 
             if (i < e1) {
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    v[u][g] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + i + g * PER));
-                    c[u][g] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(colw + i + g * PER));
+                    if (ABL == 3) {
+                        v[u][g] = VT{} + V(i & 7);
+                        c[u][g] = IT{};
+                    } else {
+                        v[u][g] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + i + g * PER));
+                        c[u][g] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(colw + i + g * PER));
+                    }
                 }
             }
         }
@@ -127,8 +135,10 @@ __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t 
                     VT p;
 #pragma unroll
                     for (int k = 0; k < PER; ++k)
-                        p[k] = v[u][g][k] * xs[c[u][g][k]];
-                    if (NTS)
+                        p[k] = ABL == 1 ? v[u][g][k] * V(c[u][g][k]) : v[u][g][k] * xs[c[u][g][k]];
+                    if (ABL == 2)
+                        sink += p;
+                    else if (NTS)
                         __builtin_nontemporal_store(p, reinterpret_cast<VT *>(prod + i + g * PER));
                     else
                         *reinterpret_cast<VT *>(prod + i + g * PER) = p;
@@ -136,6 +146,8 @@ __global__ __launch_bounds__(1024) void k_mul(const V *__restrict__ x, uint32_t 
             }
         }
     }
+    if (ABL == 2 && sink[0] == V(1.2345))
+        prod[0] = sink[1];
 }
 
 // pass 2: blockIdx.x = panel; segment (w, p) = entries [(w P + p) L, +L), L a multiple of PER.
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(1024) void k_acc_pipe(const V *__restrict__ prod, c
             y[r0 + i] = (V)ys[i];
 }
 
-template <typename V, int U, int D, int G1 = 1, int G2 = 1, bool NTS = true, bool PIPE = false>
+template <typename V, int U, int D, int G1 = 1, int G2 = 1, bool NTS = true, bool PIPE = false, int ABL = 0>
 static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint32_t L, bool check)
 {
     constexpr int PER = 16 / sizeof(V);
@@ -376,7 +388,7 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
     hipLaunchKernelGGL(k_initx<V>, dim3(4096), dim3(256), 0, 0, n, x);
     CHECK(hipDeviceSynchronize());
     const size_t lds1 = W * sizeof(V), lds2 = R * 8;
-    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mul<V, U, G1, NTS>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mul<V, U, G1, NTS, ABL>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mul_pipe<V, U>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_acc_pipe<V, D>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_acc<V, D, G2>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -390,7 +402,7 @@ static void run(const char *name, uint32_t n, uint32_t nwin, uint32_t npan, uint
         if (PIPE)
             hipLaunchKernelGGL((k_mul_pipe<V, U>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
         else
-            hipLaunchKernelGGL((k_mul<V, U, G1, NTS>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
+            hipLaunchKernelGGL((k_mul<V, U, G1, NTS, ABL>), dim3(nwin), dim3(1024), lds1, 0, x, n, W, EW, colw, val, prod);
         CHECK(hipEventRecord(ev[1], 0));
         if (PIPE)
             hipLaunchKernelGGL((k_acc_pipe<V, D>), dim3(npan), dim3(1024), lds2, 0, prod, rowp, nwin, npan, L, R, n, y);
@@ -451,21 +463,20 @@ int main(int argc, char **argv)
 {
     const bool check = argc > 1 && !std::strcmp(argv[1], "check");
     if (check) {
-        run<float, 4, 8, 1, 1, true, true>("check_f32_pipe", 200000, 6, 12, 1224, true);
-        run<double, 4, 8, 1, 1, true, true>("check_f64_pipe", 200000, 12, 12, 612, true);
-        run<float, 4, 4, 1, 1, true, true>("check_f32_pipe", 200000, 6, 12, 1224, true);
+        run<float, 4, 8>("check_f32", 200000, 6, 12, 1224, true);
         return 0;
     }
     const uint32_t n = 10000000;
+    // pass-1 ablations (pass 2 runs on whatever pass 1 wrote; only pass1_ms matters)
     for (int rep = 0; rep < 2; ++rep) {
-        run<float, 4, 8>("binned_f32", n, 256, 512, 1224, false);
-        run<float, 4, 8, 1, 1, true, true>("binned_f32_pipe", n, 256, 512, 1224, false);
-        run<float, 4, 4, 1, 1, true, true>("binned_f32_pipe", n, 256, 512, 1224, false);
-        run<float, 2, 4, 1, 1, true, true>("binned_f32_pipe", n, 256, 512, 1224, false);
-        run<double, 4, 8>("binned_f64", n, 512, 512, 612, false);
-        run<double, 4, 8, 1, 1, true, true>("binned_f64_pipe", n, 512, 512, 612, false);
-        run<double, 4, 4, 1, 1, true, true>("binned_f64_pipe", n, 512, 512, 612, false);
-        run<double, 2, 4, 1, 1, true, true>("binned_f64_pipe", n, 512, 512, 612, false);
+        run<float, 4, 8>("f32_pass1", n, 256, 512, 1224, false);
+        run<float, 4, 8, 1, 1, true, false, 1>("f32_pass1_noLDS", n, 256, 512, 1224, false);
+        run<float, 4, 8, 1, 1, true, false, 2>("f32_pass1_nostore", n, 256, 512, 1224, false);
+        run<float, 4, 8, 1, 1, true, false, 3>("f32_pass1_noload", n, 256, 512, 1224, false);
+        run<double, 4, 8>("f64_pass1", n, 512, 512, 612, false);
+        run<double, 4, 8, 1, 1, true, false, 1>("f64_pass1_noLDS", n, 512, 512, 612, false);
+        run<double, 4, 8, 1, 1, true, false, 2>("f64_pass1_nostore", n, 512, 512, 612, false);
+        run<double, 4, 8, 1, 1, true, false, 3>("f64_pass1_noload", n, 512, 512, 612, false);
     }
     return 0;
 }
