@@ -19,8 +19,10 @@
 //
 // Layout (built on the GPU): entries ordered (window, panel); a segment = the entries of one
 // (window, panel) pair, padded to a multiple of PER = 16 / sizeof(V) entries so every lane's
-// group of PER entries is one 16-byte load. Pad entries: value 0, column offset 0, row offset =
-// the scratch slot `panel_rmax` (their product, possibly 0 * inf = NaN, never reaches y).
+// group of PER entries is one 16-byte load; each window's range starts on a 128-entry boundary
+// (whole 128-byte lines for pass 1's wave loads and stores). Pad entries: value 0, column offset
+// 0, row offset = the scratch slot `panel_rmax` (their product, possibly 0 * inf = NaN, never
+// reaches y).
 //   d_b_val   V[ent_pad]    values, window-major
 //   d_b_colw  u16[ent_pad]  column - window base
 //   d_b_rowp  u16[ent_pad]  row - panel base
@@ -28,10 +30,11 @@
 //   d_b_seg   u64[nwin * npan + 1]  padded segment offsets, index w * npan + p
 //   d_b_ub    u64[nunits + 1], d_b_uwin u32[nunits]: pass-1 work units (a window, or a piece of
 //             a window holding > 2x the mean entries)
-// Bytes per non-zero: fp32 4 + 2 read, 4 written, 4 + 2 read = 16; fp64 28. Measured on
-// 10M x 10M / 160M (tools/binned_probe.hip, profiles/r02_binned_probe.jsonl): fp32 0.47-0.49 ms
-// against 0.615 ms for the sweep; fp64 0.80-0.82 ms against 0.785, so the automatic choice
-// takes it for fp32 only (plan.cpp).
+// Bytes per non-zero: fp32 4 + 2 read, 4 written, 4 + 2 read = 16; fp64 28. Both passes are
+// HBM-bound (pass 1's reads and writes add up at ~6 TB/s). Measured on 10M x 10M / 160M
+// (profiles/r02_binned.jsonl): fp32 0.457-0.51 ms against 0.60-0.62 ms for the sweep; fp64
+// 0.80-0.86 ms against 0.78-0.79, so the automatic choice takes it for fp32 only (plan.cpp),
+// and not for skewed matrices (a panel of long rows would serialise pass 2's LDS adds).
 //
 // fp32 rows: products rounded to fp32 (the reference's fp32 multiply), summed in fp64, rounded
 // once. Like the sweep, the LDS adds land in timing order: y is not bitwise reproducible run to
