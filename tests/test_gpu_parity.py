@@ -265,6 +265,34 @@ def test_nan_in_unused_x_does_not_leak(torch, kernel):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_nonfinite_x_propagates_like_spmv_gold(torch, kernel, dtype):
+    """NaN, +inf and -inf in used columns of x, and explicit zero values on inf columns (0 * inf
+    = NaN): whether a row ends NaN, +inf, -inf or finite does not depend on the summation order,
+    so every kernel's rows must match spmv_gold's class exactly (csr.cpp:184-194), and the
+    finite rows stay within the tolerance."""
+    rng = np.random.default_rng(23)
+    n, m = 5_000, 40_000
+    row_ptr, col, val, x = random_csr(rng, n, m, rng.integers(0, 30, n), dtype)
+    special = rng.choice(m, 60, replace=False)
+    x[special[:20]] = np.nan
+    x[special[20:40]] = np.inf
+    x[special[40:]] = -np.inf
+    hits_inf = np.isin(col, special[20:]) & (rng.random(len(col)) < 0.3)
+    val[hits_inf] = 0  # 0 * inf = NaN in that row
+    ref = oracle.spmv_gold(row_ptr, col, val, x)
+    y, _ = run_device(torch, spmv_hw.load(dtype), row_ptr, col, val, x, m)
+    assert np.isnan(ref).sum() > 10 and np.isinf(ref).sum() > 10  # the case exercises all classes
+    assert np.array_equal(np.isnan(y), np.isnan(ref))
+    assert np.array_equal(np.isposinf(y), np.isposinf(ref)) and np.array_equal(np.isneginf(y), np.isneginf(ref))
+    fin = np.isfinite(ref)
+    keep = np.repeat(fin, np.diff(row_ptr.astype(np.int64)))  # entries of the finite rows
+    sub_rp = np.zeros(int(fin.sum()) + 1, np.int64)
+    sub_rp[1:] = np.cumsum(np.diff(row_ptr.astype(np.int64))[fin])
+    xf = np.where(np.isfinite(x), x, 0).astype(dtype)  # finite rows use no non-finite x
+    check(sub_rp.astype(np.uint32), col[keep], val[keep], xf, ref[fin], y[fin], dtype)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_unaligned_x_and_y(torch, kernel, dtype):
     """x and y given as views one element into their buffers (not 16-byte aligned): kernels
     that stage x with 16-byte loads (the binned kernel's pass 1) take their element-wise path."""
