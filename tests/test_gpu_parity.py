@@ -293,6 +293,24 @@ def test_nonfinite_x_propagates_like_spmv_gold(torch, kernel, dtype):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("shape", ["wide", "tall"])
+def test_extreme_aspect_ratios(torch, kernel, shape, dtype):
+    """wide: 1,000 rows over 10M columns (x of 80 MB, ~200 scattered entries a row: many column
+    windows / blocks, few rows); tall: 1M rows over 64 columns (x in one cache line or two)."""
+    rng = np.random.default_rng(29)
+    if shape == "wide":
+        n, m, k = 1_000, 10_000_000, 200
+    else:
+        n, m, k = 1_000_000, 64, 4
+    cols = np.sort(rng.integers(0, m, (n, k)), axis=1).astype(np.uint32).ravel()
+    row_ptr = (np.arange(n + 1, dtype=np.int64) * k).astype(np.uint32)
+    val = rng.uniform(-1, 1, n * k).astype(dtype)
+    x = rng.uniform(0, 1, m).astype(dtype)
+    y, _ = run_device(torch, spmv_hw.load(dtype), row_ptr, cols, val, x, m, expect_kernel=kernel)
+    check(row_ptr, cols, val, x, oracle.spmv_gold(row_ptr, cols, val, x), y, dtype)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_unaligned_x_and_y(torch, kernel, dtype):
     """x and y given as views one element into their buffers (not 16-byte aligned): kernels
     that stage x with 16-byte loads (the binned kernel's pass 1) take their element-wise path."""
