@@ -32,7 +32,8 @@ cpu_baseline (the oracle's restatement of spmv_gold, 1 thread, on the host of th
 parity (full-size componentwise-scaled error vs that oracle run),
 lds_xtiles (power-law, 1 GPU: the same matrix through kernel 4, the reference's dataflow with a
 block of x in LDS per workgroup -- the technique BASELINE configs 3/5 name -- timed beside the
-headline kernel), deterministic (power-law, 1 GPU: the same matrix with SPMV_SWEEP_DETERMINISTIC=1,
+headline kernel), binned (power-law, 1 GPU: the same matrix through kernel 6, the two-pass
+gather-free alternative), deterministic (power-law, 1 GPU: the same matrix with SPMV_SWEEP_DETERMINISTIC=1,
 bitwise reproducible y, timed the same way), side_configs (1 GPU: BASELINE config 2, banded
 1M x 16 fp64, and config 5, the power-law matrix in fp32, each timed the same way with its own
 roofline and oracle parity).
@@ -248,6 +249,44 @@ def lds_xtiles(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
            "gflops": round(2.0 * st["nr_nzeros"] / (ms * 1e-3) / 1e9, 3),
            "alg_GBps": round(st["algorithmic_bytes"] / (ms * 1e-3) / 1e9, 2),
            "device_bytes": st["device_bytes"], "max_rel_diff_vs_value_kernel": diff}
+    plan.destroy()
+    del y
+    torch.cuda.empty_cache()
+    return res
+
+
+def binned_side(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
+    """The same matrix through the two-pass binned kernel (SPMV_HW_KERNEL=binned: products per
+    column window, summed per row panel; 16 B per non-zero in fp32, 28 B in fp64), timed like
+    the headline: the gather-free alternative to the sweep, measured beside it."""
+    saved = os.environ.get("SPMV_HW_KERNEL")
+    os.environ["SPMV_HW_KERNEL"] = "binned"
+    try:
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, ncols, device=dev_index, stream=stream)
+    finally:
+        if saved is None:
+            os.environ.pop("SPMV_HW_KERNEL", None)
+        else:
+            os.environ["SPMV_HW_KERNEL"] = saved
+    y = torch.empty_like(y_ref)
+    for _ in range(args.warmup):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    for _ in range(args.steps):
+        plan.run(x, y, stream)
+    torch.cuda.synchronize()
+    ms, _, launches = plan.timing()
+    plan.set_timing(False)
+    diff = float(((y.double() - y_ref.double()).abs().max() / y_ref.double().abs().max().clamp_min(1e-300)).item())
+    st = plan.stats()
+    streamed = st["nr_nzeros"] * (2 * (2 * y_ref.element_size() + 2) - y_ref.element_size())
+    res = {"kernel": "k_bin_mul + k_bin_acc", "env": "SPMV_HW_KERNEL=binned", "ms_per_step": round(ms, 5),
+           "launches": launches, "gflops": round(2.0 * st["nr_nzeros"] / (ms * 1e-3) / 1e9, 3),
+           "alg_GBps": round(st["algorithmic_bytes"] / (ms * 1e-3) / 1e9, 2),
+           "streamed_bytes_per_launch": streamed,
+           "streamed_GBps": round(streamed / (ms * 1e-3) / 1e9, 2),
+           "max_rel_diff_vs_value_kernel": diff}
     plan.destroy()
     del y
     torch.cuda.empty_cache()
@@ -553,12 +592,17 @@ def main():
     graph = {"iters": args.steps, "ms_per_step": round(ms, 5), "timed": "headline (value, ms_per_step)",
              "eager_ms_per_step": round(eager_ms, 5)}
 
-    xtiles = det = None
+    xtiles = det = binned = None
     if want_xtiles:  # reported beside the headline, never fatal to it
         try:
             xtiles = lds_xtiles(lib, args, rp, col, val, x, y, ncols, local, stream)
         except Exception as e:
             xtiles = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+        if st["kernel"] != 6:
+            try:
+                binned = binned_side(lib, args, rp, col, val, x, y, ncols, local, stream)
+            except Exception as e:
+                binned = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
         if not args.no_det:
             try:
                 det = deterministic_side(lib, args, rp, col, val, x, y, ncols, local, stream)
@@ -684,6 +728,7 @@ def main():
         "strong_companion": None,
         "weak_companion": None,
         "lds_xtiles": xtiles,
+        "binned": binned,
         "deterministic": det,
         "side_configs": None,
         "host_copy": host,
