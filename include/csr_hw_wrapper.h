@@ -105,7 +105,8 @@ typedef struct spmv_plan_stats {
     int32_t format;              /* bit 0: 16- or 8-bit column offsets (per tile, kernel 0; per
                                     slot, kernel 5), bit 3: 8-bit, bit 4: 16-bit (cluster, offset)
                                     with 4 bases per tile / slot; bit 1: packed 12/8-byte sweep
-                                    entries; bit 2: lane-ordered chunks (kernel 2) */
+                                    entries; bit 2: lane-ordered chunks (kernel 2); bit 5: row-
+                                    sorted segments with 1-byte row deltas (kernel 6) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are

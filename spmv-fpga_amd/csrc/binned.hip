@@ -20,17 +20,20 @@
 // Layout (built on the GPU): entries ordered (window, panel); a segment = the entries of one
 // (window, panel) pair, padded to a multiple of PER = 16 / sizeof(V) entries so every lane's
 // group of PER entries is one 16-byte load; each window's range starts on a 128-entry boundary
-// (whole 128-byte lines for pass 1's wave loads and stores). Pad entries: value 0, column offset
-// 0, row offset = the scratch slot `panel_rmax` (their product, possibly 0 * inf = NaN, never
-// reaches y).
+// (whole 128-byte lines for pass 1's wave loads and stores). Pad (and escape) entries: value 0,
+// column offset kBinSent, for which pass 1 writes an exact +0 product (0 * x would be NaN for
+// a non-finite x); row offset 0 / delta 0 (or 255 for an escape).
 //   d_b_val   V[ent_pad]    values, window-major
 //   d_b_colw  u16[ent_pad]  column - window base
-//   d_b_rowp  u16[ent_pad]  row - panel base
+//   d_b_rowp  u16[ent_pad]  row - panel base, or (b_delta: segments sorted by row) u8 deltas
+//             from the previous entry of the segment (the first from row 0), gaps above 255
+//             bridged by escape entries (delta 255, product 0)
 //   d_b_prod  V[ent_pad]    products (scratch written by pass 1, read by pass 2)
 //   d_b_seg   u64[nwin * npan + 1]  padded segment offsets, index w * npan + p
 //   d_b_ub    u64[nunits + 1], d_b_uwin u32[nunits]: pass-1 work units (a window, or a piece of
 //             a window holding > 2x the mean entries)
-// Bytes per non-zero: fp32 4 + 2 read, 4 written, 4 + 2 read = 16; fp64 28. Both passes are
+// Bytes per non-zero: fp32 4 + 2 read, 4 written, 4 + 2 (1 with deltas) read = 16 (15); fp64
+// 28 (27). Both passes are
 // HBM-bound (pass 1's reads and writes add up at ~6 TB/s). Measured on 10M x 10M / 160M
 // (profiles/r02_binned.jsonl): fp32 0.457-0.51 ms against 0.60-0.62 ms for the sweep; fp64
 // 0.80-0.86 ms against 0.78-0.79, so the automatic choice takes it for fp32 only (plan.cpp),
@@ -40,6 +43,7 @@
 // once. Like the sweep, the LDS adds land in timing order: y is not bitwise reproducible run to
 // run (scaled error <= 1e-15 fp64 / one fp32 rounding).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -66,6 +70,28 @@ constexpr int kBinU = 4;     // pass 1: 64-lane steps of loads in flight per wav
 constexpr int kBinD = 8;     // pass 2: steps in flight per wave
 constexpr int kBinStageLoads = 10;  // pass 1: 16-B x loads per thread staging a window
 constexpr uint64_t kBinAlign = 128;  // entries: window ranges and pass-1 units start at multiples
+constexpr uint16_t kBinSent = 0xFFFF;  // column offset of a pad entry: its product is exactly +0
+                                       // (W <= 40960, so no real offset takes this value)
+
+// delta bytes of one lane's PER entries (delta layout)
+template <int PER> struct BinDelta;
+template <> struct BinDelta<4> { typedef uint32_t T; };
+template <> struct BinDelta<2> { typedef uint16_t T; };
+
+// 64-lane inclusive prefix sum (the GCN DPP sequence: row_shr 1/2/3 of the source, row_shr 4/8
+// with bank masks, row_bcast 15/31 with row masks); tools/delta_probe.hip checks it
+__device__ __forceinline__ uint32_t bin_wave_inclusive_sum(uint32_t v0)
+{
+    uint32_t v = v0;
+    v += __builtin_amdgcn_update_dpp(0u, v0, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v0, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v0, 0x113, 0xf, 0xf, true);  // row_shr:3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xe, true);   // row_shr:4, banks 1-3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xc, true);   // row_shr:8, banks 2-3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15, rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31, rows 2, 3
+    return v;
+}
 
 // Pass 1: unit u = entries [ub[u], ub[u+1]) of window uwin[u] (both multiples of PER).
 // AL: x is 16-byte aligned, so the window is staged with 16-byte loads.
@@ -140,8 +166,11 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
             if (i < e1) {
                 VT pr;
 #pragma unroll
-                for (int q = 0; q < PER; ++q)
-                    pr[q] = v[k][q] * xs[c[k][q]];
+                for (int q = 0; q < PER; ++q) {
+                    const uint16_t cq = c[k][q];
+                    const V xq = xs[cq == kBinSent ? 0 : cq];
+                    pr[q] = cq == kBinSent ? V(0) : v[k][q] * xq;
+                }
                 __builtin_nontemporal_store(pr, reinterpret_cast<VT *>(prod + i));
             }
         }
@@ -153,8 +182,11 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
 // segment masked), kBinD steps of loads in flight before the adds. The bounds of the wave's next
 // 64 segments sit in a lane table (lane l: segment 64c + l) read with readlane, so crossing a
 // segment costs no scalar load (whose wait would also drain the outstanding LDS adds).
-template <typename V>
-__global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, const uint16_t *__restrict__ rowp,
+// DELTA: `rowp` holds 1-byte row deltas (segments sorted by row, each starting from row 0); a
+// step's rows are its deltas' running sum: a 64-lane prefix sum of the lanes' PER-delta totals
+// plus the carry of the segment's earlier steps.
+template <typename V, bool DELTA>
+__global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, const void *__restrict__ rowp,
                                                    const uint64_t *__restrict__ seg,
                                                    const uint32_t *__restrict__ panel_row, uint32_t nwin,
                                                    uint32_t npan, uint32_t slots, V *__restrict__ y)
@@ -202,14 +234,22 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
         table(0);
         bounds(0, pos, end);
     }
+    typedef typename BinDelta<PER>::T DT;
+    const uint16_t *__restrict__ rows16 = reinterpret_cast<const uint16_t *>(rowp);
+    const uint8_t *__restrict__ rows8 = reinterpret_cast<const uint8_t *>(rowp);
+    uint32_t carry = 0;  // DELTA: row of the segment's last entry so far
     while (o < nmine) {
         VT v[kBinD];
         IT r[kBinD];
+        DT dl[kBinD];
         uint64_t at[kBinD], en[kBinD];
+        bool fresh[kBinD];  // DELTA: the step starts a segment (uniform)
 #pragma unroll
         for (int k = 0; k < kBinD; ++k) {
+            bool moved = false;
             while (pos >= end && o < nmine) {  // next non-empty segment (uniform)
                 ++o;
+                moved = true;
                 if (o < nmine) {
                     if ((o & 63) == 0)
                         table(o >> 6);
@@ -218,14 +258,38 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
             }
             at[k] = pos + lane * PER;
             en[k] = o < nmine ? end : 0;
+            fresh[k] = moved;
             if (at[k] < en[k]) {
                 v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + at[k]));
-                r[k] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(rowp + at[k]));
+                if (DELTA)
+                    dl[k] = __builtin_nontemporal_load(reinterpret_cast<const DT *>(rows8 + at[k]));
+                else
+                    r[k] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(rows16 + at[k]));
+            } else {
+                dl[k] = 0;
             }
             pos += STEP;
         }
 #pragma unroll
         for (int k = 0; k < kBinD; ++k) {
+            if (DELTA) {
+                if (fresh[k])
+                    carry = 0;
+                uint32_t d[PER], t = 0;
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    d[q] = ((uint32_t)dl[k] >> (8 * q)) & 0xFFu;
+                    t += d[q];
+                }
+                const uint32_t inc = bin_wave_inclusive_sum(t);
+                uint32_t row = carry + inc - t;
+                carry += (uint32_t)__builtin_amdgcn_readlane(inc, 63);
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    row += d[q];
+                    r[k][q] = (uint16_t)row;
+                }
+            }
             if (at[k] < en[k]) {
 #pragma unroll
                 for (int q = 0; q < PER; ++q)
@@ -293,19 +357,84 @@ __global__ void k_bin_scatter(const uint32_t *__restrict__ key, const uint16_t *
     rowp[d] = rowp_in[j];
 }
 
-// pad entries of every segment: value 0, column offset 0, the scratch row slot
+// escape entries before sorted entry k of the delta layout: a row gap above 255 is bridged by
+// pad entries of delta 255 (product 0), the entry itself keeps the remainder (1..255)
+__device__ __forceinline__ uint32_t bin_escapes(uint32_t gap) { return gap > 255u ? (gap - 1u) / 255u : 0u; }
+
+// sort key of the delta layout: (segment << 16) | row offset, and the entry's CSR index
+__global__ void k_bin_key64(const uint32_t *__restrict__ key, const uint16_t *__restrict__ rowp, uint64_t nnz,
+                            uint64_t *__restrict__ k64, uint32_t *__restrict__ idx)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz)
+        return;
+    k64[j] = ((uint64_t)key[j] << 16) | rowp[j];
+    idx[j] = (uint32_t)j;
+}
+
+// per sorted entry: its escape count (segments start from row 0); per segment: their sum
+__global__ void k_bin_gaps(const uint64_t *__restrict__ k64, uint64_t nnz, uint32_t *__restrict__ pads,
+                           uint32_t *__restrict__ esc)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz)
+        return;
+    const uint64_t sg = k64[k] >> 16;
+    const uint32_t row = (uint32_t)(k64[k] & 0xFFFFu);
+    const uint32_t prev = (k > 0 && (k64[k - 1] >> 16) == sg) ? (uint32_t)(k64[k - 1] & 0xFFFFu) : 0u;
+    const uint32_t e = bin_escapes(row - prev);
+    pads[k] = e;
+    if (e)
+        atomicAdd(&esc[sg], e);
+}
+
+// delta layout: sorted entry k (and the escapes before it) to its padded position
 template <typename V>
+__global__ void k_bin_scatter_delta(const uint64_t *__restrict__ k64, const uint32_t *__restrict__ idx,
+                                    const uint32_t *__restrict__ pscan, const uint64_t *__restrict__ sorted_off,
+                                    uint64_t nnz, uint32_t npan, uint32_t W, const IndexType *__restrict__ col,
+                                    const V *__restrict__ val_in, const uint64_t *__restrict__ seg,
+                                    V *__restrict__ val, uint16_t *__restrict__ colw, uint8_t *__restrict__ delta)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz)
+        return;
+    const uint64_t sg = k64[k] >> 16;
+    const uint32_t row = (uint32_t)(k64[k] & 0xFFFFu);
+    const uint64_t k0 = sorted_off[sg];
+    const uint32_t prev = k > k0 ? (uint32_t)(k64[k - 1] & 0xFFFFu) : 0u;
+    const uint32_t gap = row - prev, e = bin_escapes(gap);
+    // entries of this segment before k, plus all their escapes, plus this entry's own escapes
+    const uint64_t d = seg[sg] + (k - k0) + (uint64_t)(pscan[k] - pscan[k0]) + e;
+    for (uint32_t t = 0; t < e; ++t) {
+        val[d - e + t] = V(0);
+        colw[d - e + t] = kBinSent;
+        delta[d - e + t] = 255;
+    }
+    const uint32_t j = idx[k];
+    val[d] = val_in[j];
+    colw[d] = (uint16_t)(col[j] - (uint32_t)(sg / npan) * W);
+    delta[d] = (uint8_t)(gap - 255u * e);
+}
+
+// pad entries at the end of every segment: value 0, the sentinel column (product exactly +0),
+// row offset 0 / delta 0 (adding +0 to a row sum changes nothing: a sum that starts at +0 is
+// never -0)
+template <typename V, bool DELTA>
 __global__ void k_bin_pad(uint64_t nseg, const uint64_t *__restrict__ seg, const uint32_t *__restrict__ cnt,
-                          uint16_t scratch, V *__restrict__ val, uint16_t *__restrict__ colw,
-                          uint16_t *__restrict__ rowp)
+                          const uint32_t *__restrict__ esc, V *__restrict__ val, uint16_t *__restrict__ colw,
+                          void *__restrict__ rowp)
 {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nseg)
         return;
-    for (uint64_t d = seg[k] + cnt[k]; d < seg[k + 1]; ++d) {
+    for (uint64_t d = seg[k] + cnt[k] + (DELTA ? esc[k] : 0u); d < seg[k + 1]; ++d) {
         val[d] = V(0);
-        colw[d] = 0;
-        rowp[d] = scratch;
+        colw[d] = kBinSent;
+        if (DELTA)
+            reinterpret_cast<uint8_t *>(rowp)[d] = 0;
+        else
+            reinterpret_cast<uint16_t *>(rowp)[d] = 0;
     }
 }
 
@@ -326,8 +455,14 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
                            (uint32_t)p.nr_cols, p.b_W, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
     }
     const size_t lds2 = (size_t(p.panel_rmax) + 1) * sizeof(double);
-    launch_or_warm(warm, k_bin_acc<ValueType>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, p.d_b_prod, p.d_b_rowp,
-                   p.d_b_seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
+    if (p.b_delta)
+        launch_or_warm(warm, k_bin_acc<ValueType, true>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, p.d_b_prod,
+                       (const void *)p.d_b_rowp, p.d_b_seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels,
+                       p.panel_rmax + 1, d_y);
+    else
+        launch_or_warm(warm, k_bin_acc<ValueType, false>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, p.d_b_prod,
+                       (const void *)p.d_b_rowp, p.d_b_seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels,
+                       p.panel_rmax + 1, d_y);
     return hipGetLastError();
 }
 
@@ -412,10 +547,23 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     IndexType *d_rp = nullptr;
     uint32_t *d_key = nullptr, *d_cnt = nullptr, *d_cur = nullptr;
     uint16_t *d_rowp_tmp = nullptr;
+    // delta layout temporaries
+    uint64_t *d_k64 = nullptr, *d_k64s = nullptr, *d_soff = nullptr;
+    uint32_t *d_idx = nullptr, *d_idxs = nullptr, *d_pads = nullptr, *d_pscan = nullptr, *d_esc = nullptr;
+    void *d_tmp = nullptr;
+    auto free_delta = [&]() {
+        for (void **q : {(void **)&d_k64, (void **)&d_k64s, (void **)&d_soff, (void **)&d_idx, (void **)&d_idxs,
+                         (void **)&d_pads, (void **)&d_pscan, (void **)&d_esc, &d_tmp})
+            if (*q) {
+                (void)hipFree(*q);
+                *q = nullptr;
+            }
+    };
     auto cleanup = [&]() {
         for (void *q : {(void *)d_rp, (void *)d_key, (void *)d_cnt, (void *)d_cur, (void *)d_rowp_tmp})
             if (q)
                 (void)hipFree(q);
+        free_delta();
     };
     auto fail = [&](hipError_t e, const char *what) {
         set_error(std::string("build_binned: ") + what + ": " + hipGetErrorString(e));
@@ -442,13 +590,75 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         BN_TRY(hipMemcpyAsync(cnt.data(), d_cnt, nseg * 4, hipMemcpyDeviceToHost, s));
         BN_TRY(hipStreamSynchronize(s));
     }
+    // Delta layout (env SPMV_BIN_DELTA: 0 never, 1 always, default when its escape entries stay
+    // under 1 % of nnz): each segment sorted by row, 1-byte row deltas, pass 2 reading 1 B less
+    // per non-zero (tools/delta_probe.hip: pass 2 0.159 vs 0.180 ms on the 10M/160M fp32 shape).
+    // Sparse segments (small matrices, gaps over 255 rows) would need many escapes: u16 offsets.
+    std::vector<uint32_t> esc(nseg, 0);
+    bool delta = false;
+    {
+        const char *denv = std::getenv("SPMV_BIN_DELTA");
+        const bool never = denv && denv[0] == '0', always = denv && denv[0] == '1';
+        delta = !nnz && always;  // an empty slice: either form reads nothing
+        if (nnz && !never) {
+            BN_TRY(hipMalloc((void **)&d_k64, nnz * 8));
+            BN_TRY(hipMalloc((void **)&d_k64s, nnz * 8));
+            BN_TRY(hipMalloc((void **)&d_idx, nnz * 4));
+            BN_TRY(hipMalloc((void **)&d_idxs, nnz * 4));
+            hipLaunchKernelGGL(k_bin_key64, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_key, d_rowp_tmp,
+                               nnz, d_k64, d_idx);
+            BN_TRY(hipGetLastError());
+            int end_bit = 17;
+            while (end_bit < 64 && (1ull << (end_bit - 16)) < nseg)
+                ++end_bit;
+            size_t tb = 0;
+            BN_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_k64, d_k64s, d_idx, d_idxs, nnz, 0, end_bit, s));
+            BN_TRY(hipMalloc(&d_tmp, tb));
+            BN_TRY(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k64, d_k64s, d_idx, d_idxs, nnz, 0, end_bit, s));
+            BN_TRY(hipFree(d_k64));
+            d_k64 = nullptr;
+            BN_TRY(hipFree(d_idx));
+            d_idx = nullptr;
+            BN_TRY(hipFree(d_tmp));
+            d_tmp = nullptr;
+            BN_TRY(hipMalloc((void **)&d_pads, nnz * 4));
+            BN_TRY(hipMalloc((void **)&d_esc, std::max<uint64_t>(nseg, 1) * 4));
+            BN_TRY(hipMemsetAsync(d_esc, 0, std::max<uint64_t>(nseg, 1) * 4, s));
+            hipLaunchKernelGGL(k_bin_gaps, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_k64s, nnz, d_pads,
+                               d_esc);
+            BN_TRY(hipGetLastError());
+            BN_TRY(hipMemcpyAsync(esc.data(), d_esc, nseg * 4, hipMemcpyDeviceToHost, s));
+            BN_TRY(hipStreamSynchronize(s));
+            uint64_t total = 0;
+            for (uint32_t e : esc)
+                total += e;
+            delta = always || total * 100 <= nnz;
+            if (delta) {
+                BN_TRY(hipMalloc((void **)&d_pscan, nnz * 4));
+                tb = 0;
+                BN_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_pads, d_pscan, nnz, s));
+                BN_TRY(hipMalloc(&d_tmp, tb));
+                BN_TRY(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_pads, d_pscan, nnz, s));
+                std::vector<uint64_t> soff(nseg + 1, 0);
+                for (uint64_t k = 0; k < nseg; ++k)
+                    soff[k + 1] = soff[k] + cnt[k];
+                BN_TRY(hipMalloc((void **)&d_soff, (nseg + 1) * 8));
+                BN_TRY(hipMemcpyAsync(d_soff, soff.data(), (nseg + 1) * 8, hipMemcpyHostToDevice, s));
+                BN_TRY(hipStreamSynchronize(s));
+            } else {
+                free_delta();
+                std::fill(esc.begin(), esc.end(), 0u);
+            }
+        }
+    }
+    p.b_delta = delta;
     // padded segment offsets (window-major), then the pass-1 units
     // Each window's range also starts on a 128-entry boundary (the last segment of the window
     // takes the extra pad entries): pass 1's 1-KiB wave loads and stores then cover whole
     // 128-byte lines instead of straddling them (partial-line stores).
     std::vector<uint64_t> seg(nseg + 1, 0);
     for (uint64_t k = 0; k < nseg; ++k) {
-        seg[k + 1] = seg[k] + (cnt[k] + PER - 1) / PER * PER;
+        seg[k + 1] = seg[k] + (uint64_t(cnt[k]) + esc[k] + PER - 1) / PER * PER;
         if ((k + 1) % P == 0)
             seg[k + 1] = (seg[k + 1] + kBinAlign - 1) / kBinAlign * kBinAlign;
     }
@@ -484,16 +694,25 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     BN_TRY(hipMalloc((void **)&p.d_b_val, alloc * sizeof(ValueType)));
     BN_TRY(hipMalloc((void **)&p.d_b_prod, alloc * sizeof(ValueType)));
     BN_TRY(hipMalloc((void **)&p.d_b_colw, alloc * 2));
-    BN_TRY(hipMalloc((void **)&p.d_b_rowp, alloc * 2));
-    if (nnz) {
+    BN_TRY(hipMalloc((void **)&p.d_b_rowp, alloc * (delta ? 1 : 2)));
+    if (nnz && delta) {
+        hipLaunchKernelGGL((k_bin_scatter_delta<ValueType>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s,
+                           d_k64s, d_idxs, d_pscan, d_soff, nnz, P, (uint32_t)W, d_col_src, d_val_src, p.d_b_seg,
+                           p.d_b_val, p.d_b_colw, reinterpret_cast<uint8_t *>(p.d_b_rowp));
+        BN_TRY(hipGetLastError());
+        BN_TRY(hipMemcpyAsync(d_esc, esc.data(), nseg * 4, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL((k_bin_pad<ValueType, true>), dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, nseg,
+                           p.d_b_seg, d_cnt, d_esc, p.d_b_val, p.d_b_colw, (void *)p.d_b_rowp);
+        BN_TRY(hipGetLastError());
+    } else if (nnz) {
         BN_TRY(hipMalloc((void **)&d_cur, nseg * 4));
         BN_TRY(hipMemsetAsync(d_cur, 0, nseg * 4, s));
         hipLaunchKernelGGL((k_bin_scatter<ValueType>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_key,
                            d_rowp_tmp, d_col_src, d_val_src, nnz, P, (uint32_t)W, p.d_b_seg, d_cur, p.d_b_val,
-                           p.d_b_colw, p.d_b_rowp);
+                           p.d_b_colw, reinterpret_cast<uint16_t *>(p.d_b_rowp));
         BN_TRY(hipGetLastError());
-        hipLaunchKernelGGL((k_bin_pad<ValueType>), dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, nseg,
-                           p.d_b_seg, d_cnt, (uint16_t)rmax_used, p.d_b_val, p.d_b_colw, p.d_b_rowp);
+        hipLaunchKernelGGL((k_bin_pad<ValueType, false>), dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, nseg,
+                           p.d_b_seg, d_cnt, (const uint32_t *)nullptr, p.d_b_val, p.d_b_colw, (void *)p.d_b_rowp);
         BN_TRY(hipGetLastError());
     }
     BN_TRY(hipStreamSynchronize(s));

@@ -664,8 +664,8 @@ uint64_t spmv_plan::device_bytes() const
         return nnz * (2 + sizeof(ValueType)) + (nkpairs + 1) * 4 + nkpairs * (4 + 2 + sizeof(ValueType)) +
                (uint64_t(nr_rows) + 1) * 4 + (nchunks + 1) * 4 + nunits * 8 + 4;
     if (kernel == kKernelBinned)  // entries (value, 2 offsets), products, segments, units, panels
-        return ent_pad * (2 * sizeof(ValueType) + 4) + (uint64_t(b_nwin) * npanels + 1) * 8 + (b_nunits + 1) * 12 +
-               (npanels + 1) * 4;
+        return ent_pad * (2 * sizeof(ValueType) + 2 + (b_delta ? 1 : 2)) + (uint64_t(b_nwin) * npanels + 1) * 8 +
+               (b_nunits + 1) * 12 + (npanels + 1) * 4;
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
@@ -864,7 +864,8 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->blocks = p->kernel == kKernelBlocked ? (uint32_t)((uint64_t(p->nr_cols) + p->fpga_width - 1) / p->fpga_width) : 1;
     st->format = (p->kernel == kKernelSlices && p->slice_off_bytes < 4 ? 1 : 0) | (p->slice_clustered ? 16 : 0) |
                  (p->kernel == kKernelSlices && p->slice_off_bytes == 1 ? 8 : 0) | (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) |
-                 (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0);
+                 (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0) |
+                 (p->kernel == kKernelBinned && p->b_delta ? 32 : 0);
     return 0;
 }
 

@@ -137,7 +137,8 @@ struct spmv_plan {
     uint64_t b_nunits = 0;             // pass-1 work units
     ValueType *d_b_val = nullptr;
     uint16_t *d_b_colw = nullptr;      // column - window base
-    uint16_t *d_b_rowp = nullptr;      // row - panel base (pad entries: the scratch slot)
+    void *d_b_rowp = nullptr;          // u16 row - panel base, or (b_delta) u8 row deltas
+    bool b_delta = false;              // segments sorted by row, 1-byte deltas (binned.hip)
     ValueType *d_b_prod = nullptr;     // products, written by pass 1 and read by pass 2
     uint64_t *d_b_seg = nullptr;       // padded segment offsets [b_nwin * npanels + 1]
     uint64_t *d_b_ub = nullptr;        // pass-1 unit boundaries [b_nunits + 1]

@@ -29,9 +29,9 @@ def torch():
 
 
 KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "blocked", "slices", "slices_wide",
-           "binned"]
+           "binned", "binned_delta", "binned_u16"]
 KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "sweep_det": 2, "gold": 1, "blocked": 4,
-             "slices": 5, "slices_wide": 5, "binned": 6}
+             "slices": 5, "slices_wide": 5, "binned": 6, "binned_delta": 6, "binned_u16": 6}
 
 
 @pytest.fixture(params=KERNELS)
@@ -42,7 +42,9 @@ def kernel(request, monkeypatch):
     "sweep_unpacked" the sweep on 14-byte entries (SPMV_SWEEP_PACKED=0), the layout used when a
     chunk of a panel spans >= 65536 columns; "sweep_det" the deterministic sweep
     (SPMV_SWEEP_DETERMINISTIC=1); "slices_wide" the slice kernel with 32-bit columns
-    (SPMV_SLICE_NARROW=0); "binned" the two-pass propagation-blocking kernel (binned.hip)."""
+    (SPMV_SLICE_NARROW=0); "binned" the two-pass propagation-blocking kernel (binned.hip) with its
+    automatic row-offset form, "binned_delta" / "binned_u16" with 1-byte deltas / u16 offsets
+    forced (SPMV_BIN_DELTA=1 / 0)."""
     monkeypatch.setenv("SPMV_HW_KERNEL", request.param.split("_")[0])
     if request.param == "tiles_wide":
         monkeypatch.setenv("SPMV_TILE_NARROW", "0")
@@ -52,6 +54,10 @@ def kernel(request, monkeypatch):
         monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
     if request.param == "slices_wide":
         monkeypatch.setenv("SPMV_SLICE_NARROW", "0")
+    if request.param == "binned_delta":  # row-sorted segments with 1-byte deltas, escapes and all
+        monkeypatch.setenv("SPMV_BIN_DELTA", "1")
+    if request.param == "binned_u16":  # u16 row offsets
+        monkeypatch.setenv("SPMV_BIN_DELTA", "0")
     return request.param
 
 
@@ -78,6 +84,8 @@ def run_device(torch, lib, row_ptr, col, val, x, nr_cols, poison=True, expect_ke
             assert not stats["format"] & 1
         if expect_kernel == "sweep_unpacked":
             assert not stats["format"] & 2
+        if expect_kernel in ("binned_delta", "binned_u16"):
+            assert bool(stats["format"] & 32) == (expect_kernel == "binned_delta")
     return out, stats
 
 
