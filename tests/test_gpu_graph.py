@@ -107,3 +107,36 @@ def test_plan_run_is_capturable_into_a_torch_graph(torch, kernel):
     err = np.abs(x.cpu().numpy() - xh).max()
     assert err <= 1e-12, err
     plan.destroy()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_distinct_plans_run_concurrently_on_two_streams(torch, dtype):
+    """Plan-owned scratch (the split sweep's partial sums, the binned kernel's products) belongs
+    to one plan: two plans of the same matrix -- the sweep and the binned kernel -- launched on
+    two streams at once, repeatedly, each give the oracle's y."""
+    import os
+    lib = spmv_hw.load(dtype)
+    rp, col, val, x = _problem(lib, 1_000_000, 16_000_000)
+    n = x.numel()
+    plans = []
+    for kern in ("sweep", "binned"):
+        os.environ["SPMV_HW_KERNEL"] = kern
+        try:
+            plans.append(spmv_hw.Plan.from_device(lib, rp, col, val, n))
+        finally:
+            os.environ.pop("SPMV_HW_KERNEL", None)
+    assert [p.stats()["kernel"] for p in plans] == [2, 6]
+    ys = [torch.full((n,), float("nan"), dtype=x.dtype, device="cuda") for _ in plans]
+    streams = [torch.cuda.Stream() for _ in plans]
+    torch.cuda.synchronize()
+    for _ in range(10):
+        for p, y, s in zip(plans, ys, streams):
+            p.run(x, y, s)
+    torch.cuda.synchronize()
+    rp_h, c_h, v_h, x_h = _host(rp, col, val, x)
+    rp_h, c_h = rp_h.view(np.uint32), c_h.view(np.uint32)
+    ref = oracle.spmv_gold(rp_h, c_h, v_h, x_h)
+    for p, y in zip(plans, ys):
+        err = oracle.scaled_error(rp_h, c_h, v_h, x_h, ref, y.cpu().numpy())
+        assert err <= TIGHT[np.dtype(dtype)], (p.stats()["kernel"], err)
+        p.destroy()
