@@ -522,13 +522,14 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             if (p->locality < 0.3)
                 kernel = kKernelSweep;
         }
-        // fp32, scattered, x of >= 20 MB: the two-pass binned kernel (binned.hip) streams 16 B
-        // per non-zero instead of gathering x lines. Measured on the power-law generator
+        // fp32, scattered, x of >= 20 MB: the two-pass binned kernel (binned.hip) streams 15-16 B
+        // per non-zero instead of gathering x lines (skewed matrices excepted, build_binned). Measured on the power-law generator
         // (profiles/r02_binned.jsonl, profiles/r02_strong_binned.jsonl): square n x n, 16n nnz:
         // 4M 0.203 vs 0.199 ms (sweep), 6M 0.317 vs 0.374, 10M 0.457 vs 0.616, 20M 0.964 vs
         // 1.450; row slices of the 10M x 10M matrix (x stays 40 MB): 5M rows / 80M nnz 0.251
-        // vs 0.312, 2.5M / 40M 0.144 vs 0.178, 1.25M / 20M 0.093 vs 0.106. In fp64 (28 B per
-        // non-zero) the sweep stays as fast or faster (10M: 0.79-0.82 vs 0.79; slices slower).
+        // vs 0.312, 2.5M / 40M 0.144 vs 0.178, 1.25M / 20M 0.093 vs 0.106. In fp64 (27-28 B per
+        // non-zero) the sweep stays as fast or faster (10M: binned 0.80-0.86 vs 0.78-0.80 ms;
+        // slices slower).
         // Its pass 2 adds in timing order; SPMV_SWEEP_DETERMINISTIC=1 asks for fixed bits, which
         // the turn-ordered sweep gives, so the switch keeps the sweep.
         const char *det = std::getenv("SPMV_SWEEP_DETERMINISTIC");
