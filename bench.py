@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--extras-timeout", type=float, default=420.0,
                     help="seconds the reported-only fields after the measurement may take before the "
                          "line is printed without them")
+    ap.add_argument("--extras-timeout-status", type=int, default=0,
+                    help="exit status after the watchdog printed the line (the line stays valid: it "
+                         "carries `extras_timeout`; set e.g. 3 to make a hang visible to an exit-code check)")
     ap.add_argument("--no-det", action="store_true",
                     help="skip the deterministic-sweep side line (SPMV_SWEEP_DETERMINISTIC=1)")
     ap.add_argument("--no-xtiles", action="store_true",
@@ -380,13 +383,29 @@ def side_config(args, name, dev, stream):
                         "frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                         "alg_bytes_per_launch": alg},
            "parity": {"max_scaled_err": err, "tol": tol, "pass": bool(err <= tol)}}
+    res["roofline"]["traffic"] = None
     if st["kernel"] == 6 and name == "config5":
         # PMC traffic of the two binned passes on this matrix (profiles/r02_binned_pmc.json)
         try:
             pmc = json.load(open(os.path.join(ROOT, "profiles", "r02_binned_pmc.json")))
             res["roofline"]["traffic"] = pmc["f32"]["hbm_bytes_per_spmv"]
         except Exception:
-            res["roofline"]["traffic"] = None
+            pass
+    elif name == "config2":
+        # PMC traffic of this kernel on this matrix (profiles/traffic.json, key banded_f64), used
+        # only when it was recorded for the kernel the plan chose
+        try:
+            tr = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))["banded_f64"]
+            if tr.get("nnz") == st["nr_nzeros"] and tr["kernel"].split("<")[0] == names.get(st["kernel"]):
+                res["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+        except Exception:
+            pass
+    # the fraction of HBM peak the kernel's MEASURED bytes move at: the algorithmic `frac` charges
+    # compulsory CSR bytes (12 B/nnz fp64), which a compressed layout (e.g. 9 B/nnz narrow tiles)
+    # does not read, so `frac` can exceed what the memory system did; `frac_traffic` cannot
+    if res["roofline"]["traffic"]:
+        res["roofline"]["achieved_traffic"] = round(res["roofline"]["traffic"] / (kernel_ms * 1e-3) / 1e9, 2)
+        res["roofline"]["frac_traffic"] = round(res["roofline"]["achieved_traffic"] / HBM_PEAK_GBPS, 4)
     plan.destroy()
     del rp, col, val, x, y
     torch.cuda.empty_cache()
@@ -719,6 +738,8 @@ def main():
                      "peak_measured": stream_peak,
                      "frac_of_measured": round(achieved / stream_peak, 4) if stream_peak else None,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "frac_traffic": (round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                                      if traffic and kernel_ms > 0 else None),
                      "kernel": kname, "kernel_ms": round(kernel_ms, 5), "l2": l2,
                      "kernel_launches": launches, "alg_bytes_per_launch": alg_local},
         "cpu_baseline": None,
@@ -750,7 +771,7 @@ def main():
     def on_timeout():
         emit(f"extras still running after {args.extras_timeout} s; line printed without them")
         sys.stdout.flush()
-        os._exit(0)
+        os._exit(args.extras_timeout_status)
 
     watchdog = threading.Timer(args.extras_timeout, on_timeout)
     watchdog.daemon = True

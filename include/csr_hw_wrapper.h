@@ -111,12 +111,12 @@ typedef struct spmv_plan_stats {
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are
  * rebased to d_row_ptr[0]). The CSR arrays are only read; the plan owns its own copies. */
-int spmv_plan_create_device(spmv_plan **plan, int device, IndexType nr_rows, IndexType nr_cols,
-                            IndexType nr_nzeros, const IndexType *d_row_ptr,
+int spmv_plan_create_device(spmv_plan **plan, int device, uint32_t nr_rows, uint32_t nr_cols,
+                            uint32_t nr_nzeros, const IndexType *d_row_ptr,
                             const IndexType *d_col_ind, const ValueType *d_values, void *stream);
 /* Build a plan from rows [row_begin, row_end) of a host CSR matrix. */
 int spmv_plan_create_host(spmv_plan **plan, int device, const csr_matrix *matrix,
-                          IndexType row_begin, IndexType row_end);
+                          uint32_t row_begin, uint32_t row_end);
 /* d_y[0:nr_rows) = A * d_x  (overwrite; empty rows get 0). Asynchronous on `stream`. Enqueues
  * only kernels and memsets (when timing is off), so callers may capture it into their own
  * hipGraph, e.g. an iterative solver's SpMV + update + RCCL all-gather step.
@@ -152,7 +152,7 @@ void spmv_plan_destroy(spmv_plan *plan);
 /* nnz-balanced contiguous row partition into `units` slices: bounds[0]=0, bounds[units]=nr_rows,
  * slice u = rows [bounds[u], bounds[u+1]) with ~nnz/units non-zeros each (the
  * reference's S1 rule, csr_hw.cpp:459, without the FPGA alignment rules S2/S3). Host only. */
-int spmv_partition_rows(const IndexType *row_ptr, IndexType nr_rows, int units, IndexType *bounds);
+int spmv_partition_rows(const IndexType *row_ptr, uint32_t nr_rows, int units, IndexType *bounds);
 
 /* ---------------- Part 4: one process, several GPUs, RCCL exchange ----------
  * A spmv_mgpu splits a host CSR matrix into nnz-balanced row slices, one per device (the
@@ -186,7 +186,7 @@ void spmv_mgpu_destroy(spmv_mgpu *mg);
  * only. spmv_mgpu_set_x_device takes rank 0's x already on its device. */
 int spmv_mgpu_unique_id(unsigned char *id128);
 int spmv_mgpu_create_rank(spmv_mgpu **mg, int rank, int nranks, const unsigned char *id128, int device,
-                          const IndexType *bounds, IndexType nr_cols, const spmv_plan *plan);
+                          const IndexType *bounds, uint32_t nr_cols, const spmv_plan *plan);
 int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x);
 /* device address of this process's y (rank 0's y for a gather / reduce; the local x = y after
  * an all-gather), for callers that keep y on the GPU */
@@ -195,20 +195,20 @@ int spmv_mgpu_y_device(spmv_mgpu *mg, int exchange, ValueType **d_y);
 /* ---------------- synthetic inputs (bench/test infrastructure) ---------------- */
 /* Banded: n x n, `width` non-zeros per row, columns [clamp(i - width/2, 0, n - width), +width),
  * values U(-1,1) from splitmix64(seed). Writes d_row_ptr[n+1], d_col[n*width], d_val. */
-int spmv_gen_banded(IndexType n, IndexType width, uint64_t seed, IndexType *d_row_ptr,
+int spmv_gen_banded(uint32_t n, uint32_t width, uint64_t seed, IndexType *d_row_ptr,
                     IndexType *d_col, ValueType *d_val, void *stream);
 /* Power-law row lengths (host): l_i = clamp(floor(s * u_i^-1/2), 1, max_len), s bisected so that
  * sum(l) == nnz exactly (residual spread as +-1 over the last rows). Writes h_row_ptr[n+1]. */
-int spmv_gen_powerlaw_row_ptr(IndexType n, uint64_t nnz, IndexType max_len, uint64_t seed,
+int spmv_gen_powerlaw_row_ptr(uint32_t n, uint64_t nnz, uint32_t max_len, uint64_t seed,
                               IndexType *h_row_ptr, double *scale_out);
 /* Fill columns/values of rows [0,n) given d_row_ptr (device): row i with l non-zeros splits
  * [0,m) into l integer strata [floor(j*m/l), floor((j+1)*m/l)) and draws entry j uniformly in
  * stratum j (hash(seed,i,j)): columns strictly increase and spread over [0,m) (needs l <= m).
  * Values U(-1,1). Row i's entries depend only on (seed, i + row_offset, l, m). */
-int spmv_gen_fill(IndexType n, IndexType m, uint64_t seed, uint64_t row_offset,
+int spmv_gen_fill(uint32_t n, uint32_t m, uint64_t seed, uint64_t row_offset,
                   const IndexType *d_row_ptr, IndexType *d_col, ValueType *d_val, void *stream);
 /* d_x[i] = lo + (hi-lo)*u_i, u_i = splitmix64(seed, i + offset) in [0,1). */
-int spmv_gen_vector(IndexType n, uint64_t seed, uint64_t offset, double lo, double hi,
+int spmv_gen_vector(uint32_t n, uint64_t seed, uint64_t offset, double lo, double hi,
                     ValueType *d_x, void *stream);
 
 /* ---------------- Part 3: fast matrix reader (host only) ----------------
@@ -229,8 +229,13 @@ void spmv_free_csr(csr_matrix *matrix);
 #ifdef __cplusplus
 }
 #if defined(SPMV_USE_CALLER_CSR_TYPES)
-/* the caller's IndexType may be a class (ap_uint<32>): pass it to the C-ABI as its 32-bit value */
-inline int verification(IndexType nr_values, ValueType *sw_values, ValueType *hw_values, int verbose)
+/* the caller's IndexType may be a class (ap_uint<32>, passed by hidden reference under the C++
+ * ABI because of its user-provided copy constructor): a template forward converts it to the
+ * 32-bit value the C-ABI takes. For a plain uint32_t argument the non-template C-ABI function is
+ * the exact match and wins, so a caller whose IndexType is a uint32_t typedef sees no clash.
+ * Every other by-value count of this header is declared uint32_t for the same reason. */
+template <typename I>
+inline int verification(I nr_values, ValueType *sw_values, ValueType *hw_values, int verbose)
 {
     return verification((uint32_t)nr_values, sw_values, hw_values, verbose);
 }

@@ -152,6 +152,8 @@ int main() {
         create_csr_hw_x_vector(&hx, &x, hw[0]->blocks, hw[0]->nr_cols);
         spmv_hw(hw, hx, &y, bm);
         std::printf("%d %f\n", verification(y.nr_values, y.values, y.values, 0), (double)storage_overhead(hw[0]));
+        IndexType bounds[2];  // a by-value count in the caller's IndexType: converted to the ABI's uint32_t
+        std::printf("%d\n", spmv_partition_rows(m.row_ptr, m.nr_rows, 1, bounds));
         delete_csr_hw_matrix(hw); std::free(bm); delete_csr_hw_x_vector(hx);
     }
     return 0;
@@ -165,6 +167,23 @@ def test_dropin_header_compiles_and_links_against_caller_types(tmp_path):
     src = tmp_path / "dropin.cpp"
     src.write_text("#include <cstdlib>\n" + DROPIN_TU)
     exe = tmp_path / "dropin"
+    lib_dir = os.path.dirname(spmv_hw.lib_path(np.float64))
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-o", str(exe), "-L", lib_dir, "-lspmv_hw_f64", f"-Wl,-rpath,{lib_dir}"], check=True)
+    assert exe.exists()
+
+
+def test_dropin_header_with_a_plain_uint32_index_type(tmp_path):
+    """a caller whose IndexType is a plain uint32_t typedef (not a class) defines
+    SPMV_USE_CALLER_CSR_TYPES too; the caller-typed verification forward must not clash with the
+    C-ABI declaration, and the by-value counts must take its values unchanged."""
+    tu = DROPIN_TU.replace(
+        "struct IndexType { uint32_t v; IndexType() = default; IndexType(uint32_t x) : v(x) {} "
+        "operator uint32_t() const { return v; } };", "typedef uint32_t IndexType;")
+    assert "typedef uint32_t IndexType;" in tu
+    src = tmp_path / "dropin_u32.cpp"
+    src.write_text("#include <cstdlib>\n" + tu)
+    exe = tmp_path / "dropin_u32"
     lib_dir = os.path.dirname(spmv_hw.lib_path(np.float64))
     subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
                     "-o", str(exe), "-L", lib_dir, "-lspmv_hw_f64", f"-Wl,-rpath,{lib_dir}"], check=True)
