@@ -136,9 +136,10 @@ int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
  * 26-34 = no barrier, waves run at most 1-4 iterations ahead of the slowest wave of the
  * workgroup (26: 4 groups lag 1, 27: 4/2, 28: 2/2 = default, 29: 2/4, 30: 2/1, 31: 3/2,
  * 32: 1/2, 33: 1/4, 34: 2/3); 53-63: measurement-only ablations of the tools library, refused
- * here. 91 / 94 (packed or unpacked): the deterministic kernel of
- * SPMV_SWEEP_DETERMINISTIC=1 (LDS adds in a fixed order, bitwise reproducible y; 94 waits for
- * each wave's adds before the hand-over). Unpacked entries (a chunk spans >= 65536 columns):
+ * here. 94 (packed or unpacked): the deterministic kernel of
+ * SPMV_SWEEP_DETERMINISTIC=1 (LDS adds in a fixed order, bitwise reproducible y; each wave's
+ * adds complete before a release hand-over); 91: the same with a compiler-ordered hand-over
+ * (3 % faster; relies on the LDS executing a CU's requests in arrival order). Unpacked entries (a chunk spans >= 65536 columns):
  * 0/1/3/7/15/22 and the default (4 groups of 2 per barrier). Slices (kernel 5): 0 = 4 slot
  * pairs per iteration (default), 1 = 2, 2 = 7, 3 = 4 re-reading past the slice's end.
  * Blocked (kernel 4): 1 = measurement-only ablation, partials stored in compact order (wrong y). */

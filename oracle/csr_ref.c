@@ -127,6 +127,25 @@ void oracle_spmv_gold(IndexType nr_rows, const IndexType *row_ptr, const IndexTy
     }
 }
 
+/* spmv_gold's products (csr.cpp:190: val * x rounded to ValueType) summed in fp64 from 0 in
+ * CSR order, rounded to ValueType once per row. Not a reference function: it is the checker
+ * for the GPU kernels that accumulate fp32 products in fp64 (sweep, binned, slices): against it
+ * their error is fp64 reassociation only, so a tight bound holds where spmv_gold's own fp32
+ * running sum (over a 2M-entry row, say) is the less accurate side. Identical to spmv_gold for
+ * fp64. */
+void oracle_spmv_fp64acc(IndexType nr_rows, const IndexType *row_ptr, const IndexType *col_ind,
+                         const ValueType *values, const ValueType *x, ValueType *y)
+{
+    for (IndexType i = 0; i < nr_rows; i++) {
+        double acc = 0.0;
+        for (IndexType j = row_ptr[i]; j < row_ptr[i + 1]; j++) {
+            const ValueType prod = values[j] * x[col_ind[j]];
+            acc += (double)prod;
+        }
+        y[i] = (ValueType)acc;
+    }
+}
+
 /* Same arithmetic on a contiguous row range, for timing a bounded CPU sample. */
 void oracle_spmv_gold_rows(IndexType row_begin, IndexType row_end, const IndexType *row_ptr,
                            const IndexType *col_ind, const ValueType *values, const ValueType *x,

@@ -44,6 +44,7 @@ def lib(dtype=np.float64) -> ctypes.CDLL:
     L.oracle_init_vector_rand.argtypes = [vp, u32, cval]
     L.oracle_spmv_gold.argtypes = [u32, _u32p, _u32p, vp, vp, vp]
     L.oracle_spmv_gold_rows.argtypes = [u32, u32, _u32p, _u32p, vp, vp, vp]
+    L.oracle_spmv_fp64acc.argtypes = [u32, _u32p, _u32p, vp, vp, vp]
     L.oracle_spmv_fpga_order.argtypes = [u32, u32, _u32p, _u32p, vp, vp, vp, u32, ctypes.c_int]
     L.oracle_verification_errors.argtypes = [u32, vp, vp]
     L.oracle_verification_errors.restype = ctypes.c_long
@@ -88,6 +89,19 @@ def spmv_gold(row_ptr, col, val, x):
     y = np.zeros(n, dtype)
     lib(dtype).oracle_spmv_gold(n, _c(row_ptr, np.uint32), _c(col, np.uint32), _c(val, dtype),
                                 _c(x, dtype), y)
+    return y
+
+
+def spmv_fp64acc(row_ptr, col, val, x):
+    """spmv_gold's products (csr.cpp:190, rounded to the value type) summed in fp64 in CSR order,
+    rounded once per row: the arithmetic of the kernels that accumulate fp32 in fp64 up to
+    reassociation. The tight fp32 checker where spmv_gold's fp32 running sum is the loose side;
+    equal to spmv_gold for fp64."""
+    dtype = val.dtype
+    n = len(row_ptr) - 1
+    y = np.zeros(n, dtype)
+    lib(dtype).oracle_spmv_fp64acc(n, _c(row_ptr, np.uint32), _c(col, np.uint32), _c(val, dtype),
+                                   _c(x, dtype), y)
     return y
 
 

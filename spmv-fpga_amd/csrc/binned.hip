@@ -455,14 +455,21 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
                            (uint32_t)p.nr_cols, p.b_W, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
     }
     const size_t lds2 = (size_t(p.panel_rmax) + 1) * sizeof(double);
+    // variants 1 / 2 (tests): segment offsets rebased past 2^31 / 2^32, the product and row arrays
+    // rebased the other way, so pass 2 touches the same addresses through 64-bit offsets whose low
+    // word has bit 31 set (spmv_plan_set_variant)
+    const uint64_t base = p.d_b_seg_hi ? p.b_seg_base : 0;
+    const uint64_t *seg = p.d_b_seg_hi ? p.d_b_seg_hi : p.d_b_seg;
+    const ValueType *prod = reinterpret_cast<const ValueType *>(
+        reinterpret_cast<uintptr_t>(p.d_b_prod) - base * sizeof(ValueType));
+    const void *rowp = reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(p.d_b_rowp) -
+                                                      base * (p.b_delta ? 1 : 2));
     if (p.b_delta)
-        launch_or_warm(warm, k_bin_acc<ValueType, true>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, p.d_b_prod,
-                       (const void *)p.d_b_rowp, p.d_b_seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels,
-                       p.panel_rmax + 1, d_y);
+        launch_or_warm(warm, k_bin_acc<ValueType, true>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod, rowp,
+                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
     else
-        launch_or_warm(warm, k_bin_acc<ValueType, false>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, p.d_b_prod,
-                       (const void *)p.d_b_rowp, p.d_b_seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels,
-                       p.panel_rmax + 1, d_y);
+        launch_or_warm(warm, k_bin_acc<ValueType, false>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod, rowp,
+                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
     return hipGetLastError();
 }
 

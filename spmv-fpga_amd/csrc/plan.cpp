@@ -638,11 +638,11 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
                       (void *)d_sbase, (void *)d_slice_len, (void *)d_b_val, (void *)d_b_colw, (void *)d_b_rowp,
-                      (void *)d_b_prod, (void *)d_b_seg, (void *)d_b_ub, (void *)d_b_uwin})
+                      (void *)d_b_prod, (void *)d_b_seg, (void *)d_b_seg_hi, (void *)d_b_ub, (void *)d_b_uwin})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)
@@ -670,7 +670,8 @@ uint64_t spmv_plan::device_bytes() const
     if (kernel == kKernelSweep)
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
-               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * sweep_acc_bytes : 0) + nunits * 4 + (npanels + 1) * 4;
+               (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * sweep_acc_bytes : 0) + nunits * 4 + (npanels + 1) * 4 +
+               (d_panel_cnt ? npanels * 4 : 0);
     return nnz_pad * (tile_col_bytes + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
            (tile_col_bytes < 4 ? ntiles * (tile_clustered ? 16 : 4) : 0) +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;
@@ -884,10 +885,38 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
         return 1;
     }
 #endif
-    if (p->kernel == kKernelSweep)
+    if (p->kernel == kKernelSweep) {
         p->sweep_variant = variant;
-    else
+    } else if (p->kernel == kKernelBinned) {
+        // 1 / 2 (tests, same y): pass 2 reads segment offsets rebased so that they straddle 2^31 /
+        // 2^32 entries (prod and rowp rebased the other way: the same addresses), which drives the
+        // 64-bit bound widening after readlane (binned.hip, k_bin_acc) without a 2^31-entry matrix
+        if (variant > 2) {
+            set_error("spmv_plan_set_variant: binned variants are 0, 1 and 2");
+            return 1;
+        }
+        if (p->d_b_seg_hi) {
+            SPMV_TRY(hipSetDevice(p->device));
+            SPMV_TRY(hipFree(p->d_b_seg_hi));
+            p->d_b_seg_hi = nullptr;
+            p->b_seg_base = 0;
+        }
+        if (variant) {
+            SPMV_TRY(hipSetDevice(p->device));
+            const uint64_t nseg = uint64_t(p->b_nwin) * p->npanels + 1;
+            std::vector<uint64_t> h(nseg);
+            SPMV_TRY(hipMemcpy(h.data(), p->d_b_seg, nseg * 8, hipMemcpyDeviceToHost));
+            const uint64_t base = (variant == 1 ? (1ull << 31) : (1ull << 32)) - h[nseg - 1] / 2;
+            for (auto &v : h)
+                v += base;
+            SPMV_TRY(hipMalloc((void **)&p->d_b_seg_hi, nseg * 8));
+            SPMV_TRY(hipMemcpy(p->d_b_seg_hi, h.data(), nseg * 8, hipMemcpyHostToDevice));
+            p->b_seg_base = base;
+        }
+        p->variant = variant;
+    } else {
         p->variant = variant & 3;
+    }
     // a graph captured with the previous variant must not be replayed
     if (p->gexec) {
         (void)hipSetDevice(p->device);

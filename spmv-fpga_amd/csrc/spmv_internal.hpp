@@ -119,6 +119,9 @@ struct spmv_plan {
     uint32_t *d_unit_panel = nullptr;  // panel of each work unit
     uint32_t *d_panel_unit = nullptr;  // first unit of each panel [npanels + 1]
     void *d_part = nullptr;            // split > 1: nunits x (panel_rmax + 1) partial sums (accumulator type)
+    uint32_t *d_panel_cnt = nullptr;   // split > 1 with env SPMV_SWEEP_COMBINE=fused: per-panel count of
+                                       // finished pieces (the last one combines, sweep.hip
+                                       // write_panel); null (default): k_sweep_combine
     int sweep_acc_bytes = 8;           // LDS accumulator: 8 (fp64) or 4 (fp32 via CAS, env SPMV_SWEEP_ACC=32)
     uint32_t panel_rmax = 0;
     int sweep_threads = spmvhw::kSweepThreads;  // workgroup size: 1024, 512 or 256 (env SPMV_SWEEP_THREADS)
@@ -141,6 +144,8 @@ struct spmv_plan {
     bool b_delta = false;              // segments sorted by row, 1-byte deltas (binned.hip)
     ValueType *d_b_prod = nullptr;     // products, written by pass 1 and read by pass 2
     uint64_t *d_b_seg = nullptr;       // padded segment offsets [b_nwin * npanels + 1]
+    uint64_t *d_b_seg_hi = nullptr;    // variants 1 / 2 (tests): d_b_seg + b_seg_base, read by pass 2
+    uint64_t b_seg_base = 0;           // with prod / rowp rebased by -b_seg_base (same addresses)
     uint64_t *d_b_ub = nullptr;        // pass-1 unit boundaries [b_nunits + 1]
     uint32_t *d_b_uwin = nullptr;      // window of each pass-1 unit
     double bin_skew_limit = 0.0;       // automatic choice: give up (rc 2) when a panel holds more than

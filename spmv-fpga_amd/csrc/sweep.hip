@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 
 #include "spmv_internal.hpp"
 
@@ -140,20 +141,57 @@ __device__ __forceinline__ void loadv(const V *__restrict__ v, uint64_t e, V (&o
 }
 
 // A unit's y: stored when the panel is one unit; a panel cut into pieces has each piece store
-// its fp64 partial sums (its column range) into part[unit * stride + i], and k_sweep_combine
-// adds the pieces of every row in piece order (deterministic, one rounding).
+// its fp64 partial sums (its column range) into part[unit * stride + i]. The pieces of a panel
+// are then added per row in piece order (deterministic, one rounding) -- by k_sweep_combine, a
+// second kernel (default), or (pcnt != null, env SPMV_SWEEP_COMBINE=fused) by the piece that
+// finishes last: each piece
+// publishes its partials (agent-scope release: they leave its XCD's L2), bumps the panel's
+// counter, and the one that sees pieces - 1 acquires, sums every piece's partials in piece order
+// and stores y, then re-arms the counter for the next launch (runs of one plan are ordered). The
+// sums are those of k_sweep_combine, bit for bit. It saves the second launch but serialises the
+// slab reads on one workgroup per panel: slower here (see build_sweep).
 template <typename V, int T, typename A>
 __device__ __forceinline__ void write_panel(const A *__restrict__ ylds, uint32_t R, V *__restrict__ y,
-                                            uint32_t pieces, A *__restrict__ part, uint32_t stride)
+                                            uint32_t pieces, A *__restrict__ part, uint32_t stride,
+                                            uint32_t u0, uint32_t *__restrict__ pcnt)
 {
     if (pieces == 1) {
         for (uint32_t i = threadIdx.x; i < R; i += T)
             y[i] = V(ylds[i]);
-    } else {
-        A *dst = part + (uint64_t)blockIdx.x * stride;
-        for (uint32_t i = threadIdx.x; i < R; i += T)
-            dst[i] = ylds[i];
+        return;
     }
+    A *dst = part + (uint64_t)blockIdx.x * stride;
+    for (uint32_t i = threadIdx.x; i < R; i += T)
+        dst[i] = ylds[i];
+    if (!pcnt)
+        return;
+    // the hand-off of cdna_hip_programming.md (in-launch split-K reduction): every wave drains its
+    // stores, one lane releases at agent scope (the XCD L2's dirty lines written back) and draws
+    // the ticket; the last arriver's lane 0 acquires, then all waves read the slabs
+    __shared__ uint32_t last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pieces - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last)
+        return;
+    const A *src = part + (uint64_t)u0 * stride;
+    for (uint32_t i = threadIdx.x; i < R; i += T) {
+        A acc = src[i];
+        for (uint32_t t = 1; t < pieces; ++t)
+            acc += src[(uint64_t)t * stride + i];
+        y[i] = V(acc);
+    }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // y[r0 + i] = sum over the panel's pieces u (in order) of part[u * stride + i]; panels of one
@@ -185,7 +223,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
     const uint32_t *__restrict__ col, const uint16_t *__restrict__ row, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
-    A *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
+    A *__restrict__ part, uint32_t stride, uint32_t *__restrict__ pcnt, const V *__restrict__ x,
+    V *__restrict__ y)
 {
     typedef typename EntryVec<E>::C CV;
     typedef typename EntryVec<E>::R RV;
@@ -231,7 +270,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
             __syncthreads();
     }
     __syncthreads();
-    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
+    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
 }
 
 // Packed entries (12 B instead of 14 B): rc = (row_in_panel << 16) | (column - chunk_base),
@@ -245,7 +284,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
-    A *__restrict__ part, uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
+    A *__restrict__ part, uint32_t stride, uint32_t *__restrict__ pcnt, const V *__restrict__ x,
+    V *__restrict__ y)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -351,7 +391,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     if constexpr (ABL == 8 || ABL == 9)
         lds_add(&ylds[R], sink);
     __syncthreads();
-    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
+    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
 }
 
 // Deterministic form (env SPMV_SWEEP_DETERMINISTIC=1): the same plan, layout and gathers as
@@ -368,17 +408,18 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
 // the entry loads of i + 4 before it waits for the token, so two iterations of gathers stay in
 // flight while the waves take turns (the loop body is unrolled 6 times -- 2 entry buffers x 3
 // gathered buffers -- so that no register with a load in flight is ever copied).
-// ORD = 1: the token store follows the adds' issue (compiler ordering only): the LDS executes a
-// CU's requests in arrival order and each wave's in program order, so the next wave, which can
-// only issue its adds after it has read the token, adds after. ORD = 0: the adds complete
-// (lgkmcnt 0) before a release store (3 % slower, profiles/r02_ab_variants.jsonl r02w).
+// ORD = 0 (default): the wave's adds complete (lgkmcnt 0) before a release store of the token,
+// and the next wave acquires it before its adds: the order follows from the memory model alone
+// (3 % slower than ORD 1, profiles/r02_ab_variants.jsonl r02w). ORD = 1 (variant 91, kept for
+// measurements): the token store follows the adds' issue (compiler ordering only), which is
+// correct only if the LDS executes a CU's requests in arrival order -- observed, not documented.
 // PK: packed 12-byte entries (rc + chunk base); otherwise the 14-byte form (s_col, s_row).
 template <typename V, int T, int Q, bool PK, int ORD, typename A = double>
 __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
     const uint32_t *__restrict__ col, const uint32_t *__restrict__ cbase, const uint16_t *__restrict__ srow16,
     const V *__restrict__ val, const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit, A *__restrict__ part,
-    uint32_t stride, const V *__restrict__ x, V *__restrict__ y)
+    uint32_t stride, uint32_t *__restrict__ pcnt, const V *__restrict__ x, V *__restrict__ y)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -497,7 +538,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
     const uint32_t nit = (uint32_t)((e1 - e0 + kStep - 1) / kStep);
     if (nit == 0) {
         __syncthreads();
-        write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
+        write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
         return;
     }
     EB ea, eb;
@@ -530,7 +571,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
         if ((threadIdx.x & 63) == 0)
             __hip_atomic_store(&progress[wave], 0xFFFFFFF0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __syncthreads();
-    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride);
+    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
 }
 
 // group c of G entries (a 128-entry chunk): base = min column; fails the plan's packing when the
@@ -682,16 +723,17 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(A);
     const dim3 grid((unsigned)p.nunits), block(T);
     A *part = reinterpret_cast<A *>(p.d_part);
+    uint32_t *pcnt = p.sweep_split > 1 && p.d_panel_cnt ? p.d_panel_cnt : nullptr;  // fused combine
     // Unpacked (14-B entries, used when a chunk spans >= 65536 columns): E entries per thread,
     // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
 #define SWEEP(E, Q, SYNC, NT)                                                                     \
     launch_or_warm(warm, k_spmv_sweep<ValueType, T, E, Q, SYNC, NT, A>, grid, block, lds, s, p.d_s_col,   \
-                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, d_x, d_y)
+                       p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y)
     // deterministic form (env SPMV_SWEEP_DETERMINISTIC=1, or variants 91 / 94 on any sweep plan)
 #define TURN(PK, ORD)                                                                              \
     launch_or_warm(warm, k_spmv_sweep_turn<ValueType, T, 2, PK, ORD, A>, grid, block, lds, s, p.d_s_col,          \
                    p.d_s_cbase, p.d_s_row, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, \
-                   part, p.panel_rmax + 1, d_x, d_y)
+                   part, p.panel_rmax + 1, pcnt, d_x, d_y)
 #ifdef SPMV_ABLATIONS
     // measurement only: the turn kernel's pipeline without the ordering (52: loose sync, 51: none)
     if (p.sweep_packed && p.sweep_variant == 52) {
@@ -704,7 +746,11 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     }
 #endif
     if (p.sweep_det || p.sweep_variant == kSweepTurn || p.sweep_variant == kSweepTurnOrdered) {
-        const bool ord0 = p.sweep_variant == kSweepTurnOrdered;
+        // ORD 0 (each wave's adds complete before the release hand-over) is the default of
+        // SPMV_SWEEP_DETERMINISTIC=1: its ordering follows from the memory model alone. Variant 91
+        // keeps the 3 % faster ORD 1 hand-over (compiler ordering; relies on the LDS executing a
+        // CU's requests in arrival order) for measurements.
+        const bool ord0 = p.sweep_variant != kSweepTurn;
         if (p.sweep_packed) {
             if (ord0) TURN(true, 0); else TURN(true, 1);
         } else {
@@ -716,7 +762,7 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     if (p.sweep_packed) {
 #define PKN(NT, Q, LAG, ABL)                                                                        \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
-                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, d_x, d_y)
+                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
@@ -774,7 +820,7 @@ static void launch_sweep_a(const spmv_plan &p, const ValueType *d_x, ValueType *
     case 512: launch_sweep_t<512, A>(p, d_x, d_y, s, warm); break;
     default: launch_sweep_t<1024, A>(p, d_x, d_y, s, warm); break;
     }
-    if (p.sweep_split > 1) {
+    if (p.sweep_split > 1 && !p.d_panel_cnt) {  // env SPMV_SWEEP_COMBINE=kernel
         const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
         launch_or_warm(warm, k_sweep_combine<ValueType, A>, grid, dim3(256), 0, s, p.d_panel_row, p.d_panel_unit,
                        reinterpret_cast<const A *>(p.d_part), p.panel_rmax + 1, d_y);
@@ -891,7 +937,10 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     // work units: pieces of whole chunks per panel. split mode: `split` pieces each; any panel
     // with more than twice the mean entry count (a panel holding very long rows) is cut
     // further, so that no workgroup gets more than ~2x the mean work
-    const uint32_t split = split_mode ? std::max<uint32_t>(1, (uint32_t)cus / P) : 1;
+    uint32_t split = split_mode ? std::max<uint32_t>(1, (uint32_t)cus / P) : 1;
+    // env SPMV_SWEEP_PIECES=k (experiments): k pieces per panel in split mode instead of cus / P
+    if (const char *kenv = std::getenv("SPMV_SWEEP_PIECES"); split_mode && kenv && std::atoi(kenv) > 0)
+        split = (uint32_t)std::atoi(kenv);
     const double mean = P ? double(padded) / P : 0.0;
     std::vector<uint32_t> punit(P + 1, 0);
     for (uint32_t q = 0; q < P; ++q) {
@@ -917,8 +966,20 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     uent[U] = poff[P];
     p.sweep_split = multi ? std::max<uint32_t>(split, 2) : 1;  // > 1: combine kernel needed
     p.nunits = U;
-    if (multi)
+    if (multi) {
         SPMV_TRY(hipMalloc((void **)&p.d_part, (uint64_t)U * (uint64_t(rmax_used) + 1) * acc));
+        // env SPMV_SWEEP_COMBINE=fused: the last piece of each panel combines inside the sweep
+        // launch instead of k_sweep_combine. Measured slower on the N = 8 slice of the 10M/160M
+        // matrix (0.147 vs 0.128 ms, profiles/r03_ab_sweep_combine.jsonl): the panels of a one-round
+        // launch all finish together, and each last arriver then reads its 4 x 160 KiB of partials
+        // alone (~50-70 GB/s per workgroup, MI355X_MICROARCH.md handoff-payload) where the combine
+        // kernel reads them with the whole chip; so the separate launch stays the default
+        const char *cenv = std::getenv("SPMV_SWEEP_COMBINE");
+        if (cenv && std::strcmp(cenv, "fused") == 0) {
+            SPMV_TRY(hipMalloc((void **)&p.d_panel_cnt, std::max<uint64_t>(P, 1) * 4));
+            SPMV_TRY(hipMemsetAsync(p.d_panel_cnt, 0, std::max<uint64_t>(P, 1) * 4, s));
+        }
+    }
     SPMV_TRY(hipMalloc((void **)&p.d_unit_panel, upanel.size() * 4));
     SPMV_TRY(hipMalloc((void **)&p.d_panel_unit, punit.size() * 4));
     SPMV_TRY(hipMemcpyAsync(p.d_unit_panel, upanel.data(), upanel.size() * 4, hipMemcpyHostToDevice, s));

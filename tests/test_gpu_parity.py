@@ -561,6 +561,49 @@ def test_sweep_split_pieces_match_oracle(torch, monkeypatch, dtype):
         check(row_ptr, c, v, xx, ref, y, dtype)
 
 
+def test_sweep_fused_combine_bitwise_equals_combine_kernel(torch, monkeypatch):
+    """The split sweep's combine done by the last piece of each panel (SPMV_SWEEP_COMBINE=fused)
+    adds the pieces' partials in the same piece order as the separate k_sweep_combine launch
+    (the default): with the deterministic sweep (fixed partials) the two give the
+    same bits, on every run of a plan (the per-panel counters re-arm), also with 8 pieces per
+    panel (two rounds of workgroups, SPMV_SWEEP_PIECES=8); and y matches the oracle."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
+    lib = spmv_hw.load(np.float64)
+    n_full, z_full = 10_000_000, 160_000_000
+    r0, r1 = 1_250_000, 2_500_000  # rank 1 of 8
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n_full, n_full, z_full, seed=4, row_begin=r0, row_end=r1)
+    x = spmv_hw.gen_vector(lib, n_full, seed=6)
+    ys = {}
+    for combine, pieces in (("fused", ""), ("kernel", ""), ("fused", "8"), ("kernel", "8")):
+        monkeypatch.setenv("SPMV_SWEEP_COMBINE", combine)
+        if pieces:
+            monkeypatch.setenv("SPMV_SWEEP_PIECES", pieces)
+        else:
+            monkeypatch.delenv("SPMV_SWEEP_PIECES", raising=False)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n_full)
+        st = plan.stats()
+        assert st["nr_tiles"] > 100 and st["tile_nnz"] > 0
+        runs = []
+        for _ in range(3):
+            y = torch.full((r1 - r0,), float("nan"), dtype=x.dtype, device="cuda")
+            plan.run(x, y)
+            torch.cuda.synchronize()
+            runs.append(y.cpu().numpy())
+        plan.destroy()
+        for r in runs[1:]:
+            _bitwise(runs[0], r)
+        ys[(combine, pieces)] = (st["nr_tiles"], runs[0])
+    assert ys[("fused", "8")][0] == 2 * ys[("fused", "")][0]  # 8 pieces instead of 4 per panel
+    _bitwise(ys[("fused", "")][1], ys[("kernel", "")][1])
+    _bitwise(ys[("fused", "8")][1], ys[("kernel", "8")][1])
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref = oracle.spmv_gold(row_ptr, c, v, xx)
+    for _, y in ys.values():
+        check(row_ptr, c, v, xx, ref, y, np.float64)
+
+
 # ---- gold order: bitwise the reference's spmv_gold (csr.cpp:184-194) ----
 def _bitwise(a, b):
     assert a.dtype == b.dtype and a.shape == b.shape
@@ -876,6 +919,7 @@ def test_auto_binned_skips_skewed_fp32(torch, monkeypatch):
     h = [t.cpu().numpy() for t in (rp, col, val, x)]
     row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
     ref = oracle.spmv_gold(row_ptr, c, v, xx)
+    ref64 = oracle.spmv_fp64acc(row_ptr, c, v, xx)
     for forced, want in ((None, 2), ("binned", 6)):
         if forced:
             monkeypatch.setenv("SPMV_HW_KERNEL", forced)
@@ -886,10 +930,13 @@ def test_auto_binned_skips_skewed_fp32(torch, monkeypatch):
         torch.cuda.synchronize()
         plan.destroy()
         # against spmv_gold's own fp32 running sum over the 2M-entry row: the north_star
-        # tolerance (the fp64-accumulating kernels are the more accurate side here)
+        # tolerance (the fp64-accumulating kernels are the more accurate side here) ...
         yy = y.cpu().numpy()
         assert not np.isnan(yy).any()
         assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TOL[np.dtype(np.float32)]
+        # ... and tight against the same products summed in fp64, which is
+        # what both kernels compute up to reassociation
+        assert oracle.scaled_error(row_ptr, c, v, xx, ref64, yy) <= 2e-6
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])

@@ -160,3 +160,37 @@ def test_turn_sweep_is_bitwise_reproducible(monkeypatch, variant, n, z, dtype):
     err = oracle.scaled_error(r, c, h[2], h[3], ref, ys[0].cpu().numpy())
     assert err <= (1e-12 if dtype == np.float64 else 2e-6), err
     plan.destroy()
+
+
+# ---- binned pass 2 past 2^31 / 2^32 entries without a 2^31-entry matrix ----
+
+@pytest.mark.parametrize("delta", ["1", "0"], ids=["row_deltas", "u16_rows"])
+@pytest.mark.parametrize("variant", [1, 2], ids=["straddle_2^31", "straddle_2^32"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_binned_segment_offsets_past_2_31(monkeypatch, dtype, variant, delta):
+    """Session bn5 (round 2) faulted (hipErrorIllegalAddress) on a 2.2e9-entry fp32 slice:
+    k_bin_acc reads its segment bounds with readlane, which returns a signed int, so a low word
+    >= 2^31 sign-extended into the high word of the 64-bit offset. Variants 1 / 2 rebase the
+    segment offsets by ~2^31 / ~2^32 (and the product / row arrays the other way: same
+    addresses), so half the segments lie past the boundary; y must match the oracle."""
+    import torch
+    import oracle
+    monkeypatch.setenv("SPMV_BIN_DELTA", delta)
+    lib, plan, x = _plan(monkeypatch, "binned", dtype, n=200_000, z=3_200_000)
+    st = plan.stats()
+    assert st["kernel"] == 6 and bool(st["format"] & 32) == (delta == "1")
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, 200_000, 200_000, 3_200_000, seed=4)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref = oracle.spmv_gold(r, c, h[2], h[3])
+    plan.set_variant(variant)
+    y = torch.full((200_000,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    err = oracle.scaled_error(r, c, h[2], h[3], ref, y.cpu().numpy())
+    assert err <= (1e-12 if dtype == np.float64 else 2e-6), err
+    with pytest.raises(RuntimeError, match="binned variants"):
+        plan.set_variant(3)
+    plan.set_variant(0)
+    plan.destroy()

@@ -85,6 +85,24 @@ def test_spmv_gold_matches_numpy_restatement(name, dtype, tag):
     assert np.array_equal(oracle.spmv_gold(row_ptr, col, val, x), numpy_spmv_gold(row_ptr, col, val, x))
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("dtype,tag", DTYPES)
+def test_spmv_fp64acc_matches_numpy_restatement(name, dtype, tag):
+    """oracle.spmv_fp64acc: spmv_gold's products (rounded to the value type, csr.cpp:190) summed
+    in fp64 in CSR order, rounded once -- the tight checker of the fp64-accumulating kernels.
+    Bitwise spmv_gold for fp64; for fp32 a numpy restatement in fp64 gives the same bits."""
+    path = os.path.join(GOLDEN, manifest()[name]["file"])
+    _, c, row_ptr, col, val, _ = oracle.read_csr(path, dtype)
+    x, _ = golden_arrays(name, tag)
+    y = oracle.spmv_fp64acc(row_ptr, col, val, x)
+    if np.dtype(dtype) == np.float64:
+        assert np.array_equal(y.view(np.uint8), oracle.spmv_gold(row_ptr, col, val, x).view(np.uint8))
+    prod = (val * x[col]).astype(np.float64)  # the product rounded to the value type first
+    ref = numpy_spmv_gold(row_ptr, np.arange(len(col), dtype=np.uint32), prod,
+                          np.ones(len(col), np.float64)).astype(dtype)
+    assert np.array_equal(y.view(np.uint8), ref.view(np.uint8))
+
+
 # valid reference configurations: VF >= RATIO_v (SURVEY §8c); COLS_DIV_BLOCKS by CU (util.h:41-59)
 FPGA_CONFIGS = [(32768, 2), (32768, 4), (32768, 8), (16384, 2), (16384, 8)]
 

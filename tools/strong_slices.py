@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--slices", default="ends", help="'all' slices, or first+last only")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tag", default=None, help="recorded as _setting in every line (e.g. the env under test)")
     a = ap.parse_args()
     dtype = np.float64 if a.dtype == "f64" else np.float32
     lib = spmv_hw.load(dtype)
@@ -62,7 +63,7 @@ def main():
             base = worst
         print(json.dumps({"n_gpus": N, "dtype": a.dtype, "slowest_slice_ms": round(worst, 5),
                           "aggregate_GFLOPs": round(gflops, 1), "speedup_vs_1": round(base / worst, 3),
-                          "slices": per}), flush=True)
+                          "slices": per, **({"_setting": a.tag} if a.tag else {})}), flush=True)
 
 
 if __name__ == "__main__":
