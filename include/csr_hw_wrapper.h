@@ -184,11 +184,15 @@ void spmv_mgpu_destroy(spmv_mgpu *mg);
  * [bounds[rank], bounds[rank+1]) (bounds[0..nranks], e.g. spmv_partition_rows) on `device`; the
  * handle borrows the plan. set_x / run / get_y / get_timing then work as above, collectively:
  * every rank calls them; set_x reads x on rank 0 only, get_y of a gather / reduce answers on rank 0
- * only. spmv_mgpu_set_x_device takes rank 0's x already on its device. */
+ * only. spmv_mgpu_set_x_device takes rank 0's x already on its device; it first waits for all
+ * work this process queued on that device (hipDeviceSynchronize), so an x still being written
+ * by any stream is complete before the copy. spmv_mgpu_set_x_device_on orders the copy after
+ * the producer's `stream` only (an event wait, no host wait; NULL = the legacy default stream). */
 int spmv_mgpu_unique_id(unsigned char *id128);
 int spmv_mgpu_create_rank(spmv_mgpu **mg, int rank, int nranks, const unsigned char *id128, int device,
                           const IndexType *bounds, uint32_t nr_cols, const spmv_plan *plan);
 int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x);
+int spmv_mgpu_set_x_device_on(spmv_mgpu *mg, const ValueType *d_x, void *stream);
 /* device address of this process's y (rank 0's y for a gather / reduce; the local x = y after
  * an all-gather), for callers that keep y on the GPU */
 int spmv_mgpu_y_device(spmv_mgpu *mg, int exchange, ValueType **d_y);

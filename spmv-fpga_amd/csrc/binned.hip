@@ -539,6 +539,17 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         set_error("build_binned: a panel holds long rows (skewed)");
         return 2;
     }
+    // Balanced panels still let a row of up to ~2x the mean panel entries pass the test above;
+    // its adds all land on one LDS address. The longest row is checked on its own.
+    if (p.bin_row_limit > 0.0 && P > 0) {
+        uint64_t lmax = 0;
+        for (IndexType r = 0; r < n; ++r)
+            lmax = std::max<uint64_t>(lmax, uint64_t(h_rp[r + 1]) - h_rp[r]);
+        if (double(lmax) > p.bin_row_limit * double(nnz) / P) {
+            set_error("build_binned: a row holds " + std::to_string(lmax) + " entries (long row)");
+            return 2;
+        }
+    }
     const uint64_t nseg = nwin * P;
     if (nseg >= (1ull << 28)) {
         set_error("build_binned: too many (window, panel) segments");

@@ -4,7 +4,10 @@
 // csr_hw.cpp:459). x is replicated on every GPU in use (the reference copies x into every CU's
 // BRAM, spmv.cpp:280-294). spmv_hw runs every unit's kernels, then adds each unit's y slice
 // into the caller's y_fpga (the role of accum_results, csr_hw.cpp:1531-1565, and the loop
-// csr_hw_wrapper.cpp:276-281), printing the reference's timing lines.
+// csr_hw_wrapper.cpp:276-281), printing the reference's timing lines. When the units sit on
+// distinct GPUs the slices first meet on GPU 0 over xGMI (an RCCL gather of the disjoint slices,
+// or with SPMV_HW_MERGE=reduce the literal ncclReduce(sum) of full-length partials), and one
+// D2H copy brings y to the host; SPMV_HW_MERGE=host keeps the per-GPU PCIe merge.
 #include <sys/mman.h>
 #include <sys/time.h>
 
@@ -54,9 +57,29 @@ int device_count()
 
 int unit_device(int unit) { return unit % device_count(); }
 
+// how spmv_hw merges the unit slices (env SPMV_HW_MERGE, read by create_csr_hw_matrix)
+enum { kMergeHost = 0, kMergeGather = 1, kMergeReduce = 2 };
+
+// the RCCL clique of a matrix whose units sit on distinct GPUs (owned by unit 0's handle)
+struct hw_clique {
+    spmv_mgpu *mg = nullptr;
+    int mode = kMergeGather;
+    std::vector<int> devices;       // of units 0..n-1
+    ValueType *h_full = nullptr;    // pinned staging of the whole y
+    uint64_t rows = 0;
+    ~hw_clique()
+    {
+        if (mg)
+            spmv_mgpu_destroy(mg);
+        if (h_full)
+            (void)hipHostFree(h_full);
+    }
+};
+
 struct hw_matrix_impl {
     csr_hw_matrix pub;  // must stay the first member: callers see a csr_hw_matrix*
     spmv_plan *plan = nullptr;
+    hw_clique *clique = nullptr;  // unit 0 only
     int unit = 0, device = 0;
     IndexType row_begin = 0, row_end = 0;
     // spmv_hw scratch, kept across calls: the unit's y slice on its GPU and a pinned host
@@ -133,6 +156,59 @@ void prefault(ValueType *p, uint64_t count)
 }
 
 uint64_t ceil16(uint64_t bytes) { return (bytes + 15) / 16; }
+
+// auto (default): the RCCL gather when there are >= 2 units and each has a GPU of its own, else
+// the host merge; host | gather | reduce force one (gather / reduce need one unit per GPU)
+int merge_mode(int units)
+{
+    const char *e = std::getenv("SPMV_HW_MERGE");
+    const int ndev = device_count();
+    if (!e || !*e || !std::strcmp(e, "auto"))
+        return units >= 2 && units <= ndev ? kMergeGather : kMergeHost;
+    if (!std::strcmp(e, "host"))
+        return kMergeHost;
+    const int m = !std::strcmp(e, "gather") ? kMergeGather : !std::strcmp(e, "reduce") ? kMergeReduce : -1;
+    if (m < 0)
+        die(std::string("SPMV_HW_MERGE=") + e + ": expected auto, host, gather or reduce");
+    if (units > ndev)
+        die(std::string("SPMV_HW_MERGE=") + e + " needs one unit per GPU (" + std::to_string(units) + " units, " +
+            std::to_string(ndev) + " devices)");
+    return m;
+}
+
+// adds parts[k].src into parts[k].dst on up to 16 host threads; each thread maps its part of the
+// caller's y writable first (prefault, while the DMA runs), then waits until wait_dma() returned
+struct add_part {
+    ValueType *dst;
+    const ValueType *src;
+    uint64_t count;
+};
+template <typename WaitDma>
+void host_accumulate(const std::vector<add_part> &parts, WaitDma wait_dma)
+{
+    std::atomic<bool> landed{false};
+    const char *pf_env = std::getenv("SPMV_HW_PREFAULT");
+    const bool pf = !(pf_env && pf_env[0] == '0');  // 0: let the adds take the page faults
+    auto work = [&](const add_part &q, bool wait) {
+        if (pf)
+            prefault(q.dst, q.count);
+        while (wait && !landed.load(std::memory_order_acquire))
+            std::this_thread::yield();
+        for (uint64_t i = 0; i < q.count; ++i)
+            q.dst[i] += q.src[i];
+    };
+    std::vector<std::thread> th;
+    for (size_t k = 1; k < parts.size(); ++k)
+        th.emplace_back(work, std::cref(parts[k]), true);
+    if (pf && !parts.empty())
+        prefault(parts[0].dst, parts[0].count);
+    wait_dma();
+    landed.store(true, std::memory_order_release);
+    if (!parts.empty())
+        work(parts[0], false);
+    for (auto &t : th)
+        t.join();
+}
 
 }  // namespace
 
@@ -238,6 +314,23 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         std::lock_guard<std::mutex> lk(g_mu);
         g_units_max = std::max(g_units_max, units);
     }
+    if (const int mode = merge_mode(units); mode != kMergeHost) {
+        // the clique is formed here (ncclCommInitAll), outside spmv_hw's timed region
+        auto *c = new hw_clique();
+        c->mode = mode;
+        std::vector<const spmv_plan *> plans(units);
+        for (int u = 0; u < units; ++u) {
+            c->devices.push_back(impl((*hw_matrix)[u])->device);
+            plans[u] = impl((*hw_matrix)[u])->plan;
+        }
+        c->rows = n;
+        if (mgpu_create_borrowed(&c->mg, units, c->devices.data(), bounds.data(), matrix->nr_cols, plans.data()))
+            die(std::string("create_csr_hw_matrix: RCCL merge: ") + spmv_hw_last_error());
+        check(hipSetDevice(c->devices[0]), "hipSetDevice");
+        check(hipHostMalloc((void **)&c->h_full, std::max<uint64_t>(n, 1) * sizeof(ValueType), hipHostMallocDefault),
+              "hipHostMalloc(y stage)");
+        impl((*hw_matrix)[0])->clique = c;
+    }
     // empty_rows_bitmap[block][row] (csr_hw.cpp:391-393, :340-347): inner rows live inside the
     // outer allocation, so the caller's free(outer) (main.cpp:95) releases all of it.
     const int blocks = 1;
@@ -337,6 +430,44 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         if (trace)
             std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", what, (timestamp_us() - since) / 1000);
     };
+    if (hw_clique *c = units ? impl(hw_matrix[0])->clique : nullptr) {
+        // kernels on every GPU, then the slices meet on GPU 0 over xGMI (RCCL gather, or the
+        // ncclReduce of full-length partials = accum_results' +=); "hardware" time covers both
+        std::vector<const ValueType *> xs(units);
+        for (int u = 0; u < units; ++u)
+            xs[u] = x->per_device[c->devices[u]];
+        const double hw_s = timestamp_us();
+        if (mgpu_run_on(c->mg, c->mode == kMergeReduce ? 1 : 0, xs.data()))
+            die(std::string("spmv_hw: ") + spmv_hw_last_error());
+        const double hw_exec = (timestamp_us() - hw_s) / 1000.0;
+        std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
+        if (trace) {
+            double cms = 0, ems = 0;
+            spmv_mgpu_get_timing(c->mg, &cms, &ems);
+            std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms (kernels %.3f, exchange %.3f)\n", "spmv_hw: RCCL merge",
+                         hw_exec, cms, ems);
+        }
+        // one D2H copy of the whole y from GPU 0, then the host += (accum_results into y_fpga)
+        const double ra_s = timestamp_us();
+        check(hipSetDevice(c->devices[0]), "hipSetDevice");
+        const hipStream_t s0 = unit_stream(0);
+        if (c->rows)
+            check(hipMemcpyAsync(c->h_full, mgpu_root_y(c->mg), c->rows * sizeof(ValueType), hipMemcpyDeviceToHost, s0),
+                  "hipMemcpyAsync(y)");
+        std::vector<add_part> parts;
+        const uint64_t T = c->rows < (1u << 18) ? 1 : 16;
+        for (uint64_t t = 0; t < T && c->rows; ++t) {
+            const uint64_t b = c->rows * t / T, e = c->rows * (t + 1) / T;
+            parts.push_back({y_fpga->values + b, c->h_full + b, e - b});
+        }
+        host_accumulate(parts, [&] { check(hipStreamSynchronize(s0), "y copy"); });
+        tr("spmv_hw: D2H + host accumulation", ra_s);
+        const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
+        std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
+        std::printf("Total time  : %.6f ms elapsed\n", hw_exec + ra_exec);
+        std::fflush(stdout);
+        return;
+    }
     // kernels of every unit (one stream per unit; units on different GPUs run concurrently)
     const double hw_s = timestamp_us();
     for (int u = 0; u < units; ++u) {
@@ -369,12 +500,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
               "hipMemcpyAsync(y)");
     }
     tr("spmv_hw: D2H enqueue", ra_s);
-    struct part {
-        ValueType *dst;
-        const ValueType *src;
-        uint64_t count;
-    };
-    std::vector<part> parts;  // up to 8 per unit, 16 in total
+    std::vector<add_part> parts;  // up to 8 per unit, 16 in total
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
         const uint64_t rows = m->row_end - m->row_begin;
@@ -384,34 +510,15 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
             parts.push_back({y_fpga->values + m->row_begin + b, m->h_stage + b, e - b});
         }
     }
-    std::atomic<bool> landed{false};
-    const char *pf_env = std::getenv("SPMV_HW_PREFAULT");
-    const bool pf = !(pf_env && pf_env[0] == '0');  // 0: let the adds take the page faults
-    auto work = [&](const part &q, bool wait) {
-        if (pf)
-            prefault(q.dst, q.count);
-        while (wait && !landed.load(std::memory_order_acquire))
-            std::this_thread::yield();
-        for (uint64_t i = 0; i < q.count; ++i)
-            q.dst[i] += q.src[i];
-    };
-    std::vector<std::thread> th;
-    for (size_t k = 1; k < parts.size(); ++k)
-        th.emplace_back(work, std::cref(parts[k]), true);
-    if (pf && !parts.empty())
-        prefault(parts[0].dst, parts[0].count);
-    for (int u = 0; u < units; ++u) {
-        if (impl(hw_matrix[u])->row_end == impl(hw_matrix[u])->row_begin)
-            continue;
-        check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
-        check(hipStreamSynchronize(unit_stream(u)), "y copy");
-    }
-    tr("spmv_hw: D2H done", ra_s);
-    landed.store(true, std::memory_order_release);
-    if (!parts.empty())
-        work(parts[0], false);
-    for (auto &t : th)
-        t.join();
+    host_accumulate(parts, [&] {
+        for (int u = 0; u < units; ++u) {
+            if (impl(hw_matrix[u])->row_end == impl(hw_matrix[u])->row_begin)
+                continue;
+            check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
+            check(hipStreamSynchronize(unit_stream(u)), "y copy");
+        }
+        tr("spmv_hw: D2H done", ra_s);
+    });
     tr("spmv_hw: host accumulation", ra_s);
     const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
     std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
@@ -429,6 +536,7 @@ void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix)
         if (!hw_matrix[u])
             continue;
         hw_matrix_impl *m = impl(hw_matrix[u]);
+        delete m->clique;  // before the plans it borrows
         spmv_plan_destroy(m->plan);
         if (m->d_y || m->h_stage) {
             (void)hipSetDevice(m->device);

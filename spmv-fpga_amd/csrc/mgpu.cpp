@@ -101,6 +101,7 @@ struct spmv_mgpu {
     int nranks = 0;                     // ranks of the clique (= slices)
     IndexType nr_rows = 0, nr_cols = 0;
     bool owns_plans = true;
+    bool own_x = true;                  // false: every run takes the caller's x per device
     std::vector<int> dev, rank;         // per local device: HIP device and rank
     std::vector<IndexType> bounds;      // row slice of rank r: [bounds[r], bounds[r+1])
     std::vector<const spmv_plan *> plan;
@@ -156,8 +157,10 @@ struct spmv_mgpu {
         for (int k = 0; k < 3; ++k)
             SPMV_TRY(hipEventCreate(&ev[3 * d + k]));
         const size_t xb = std::max<size_t>(nr_cols, 1) * sizeof(ValueType);
-        SPMV_TRY(hipMalloc((void **)&x[d], xb));
-        SPMV_TRY(hipMemset(x[d], 0, xb));
+        if (own_x) {
+            SPMV_TRY(hipMalloc((void **)&x[d], xb));
+            SPMV_TRY(hipMemset(x[d], 0, xb));
+        }
         if (rank[d] == 0)
             SPMV_TRY(hipMalloc((void **)&y[d], std::max<size_t>(nr_rows, 1) * sizeof(ValueType)));
         else
@@ -352,13 +355,12 @@ int spmv_mgpu_set_x(spmv_mgpu *mg, const ValueType *h_x)
     return broadcast_x(mg);
 }
 
-// the same from a device-resident x on rank 0's device
-int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x)
+// the same from a device-resident x on rank 0's device. The handle's streams are non-blocking,
+// so nothing would order the copy after the work that produced d_x: spmv_mgpu_set_x_device waits
+// for everything this process queued on rank 0's device (hipDeviceSynchronize), the _on form only
+// for the producer's `stream` (an event, no host wait; NULL = the legacy default stream).
+static int set_x_device_impl(spmv_mgpu *mg, const ValueType *d_x, bool whole_device, hipStream_t producer)
 {
-    if (!mg) {
-        set_error("spmv_mgpu_set_x_device: bad arguments");
-        return 1;
-    }
     const int r0 = mg->root_local();
     if (r0 >= 0) {
         if (!d_x) {
@@ -366,6 +368,17 @@ int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x)
             return 1;
         }
         SPMV_TRY(hipSetDevice(mg->dev[r0]));
+        if (whole_device) {
+            SPMV_TRY(hipDeviceSynchronize());
+        } else {
+            hipEvent_t e;
+            SPMV_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            hipError_t rc = hipEventRecord(e, producer);
+            if (rc == hipSuccess)
+                rc = hipStreamWaitEvent(mg->stream[r0], e, 0);
+            (void)hipEventDestroy(e);  // released once the wait has been satisfied
+            SPMV_TRY(rc);
+        }
         if (mg->nr_cols)
             SPMV_TRY(hipMemcpyAsync(mg->x[r0], d_x, size_t(mg->nr_cols) * sizeof(ValueType), hipMemcpyDeviceToDevice,
                                     mg->stream[r0]));
@@ -373,9 +386,78 @@ int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x)
     return broadcast_x(mg);
 }
 
-int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
+int spmv_mgpu_set_x_device(spmv_mgpu *mg, const ValueType *d_x)
 {
-    if (!mg || exchange < 0 || exchange > 2) {
+    if (!mg) {
+        set_error("spmv_mgpu_set_x_device: bad arguments");
+        return 1;
+    }
+    return set_x_device_impl(mg, d_x, true, nullptr);
+}
+
+int spmv_mgpu_set_x_device_on(spmv_mgpu *mg, const ValueType *d_x, void *stream)
+{
+    if (!mg) {
+        set_error("spmv_mgpu_set_x_device_on: bad arguments");
+        return 1;
+    }
+    return set_x_device_impl(mg, d_x, false, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+namespace spmvhw {
+
+int mgpu_create_borrowed(spmv_mgpu **out, int n, const int *devices, const IndexType *bounds, IndexType nr_cols,
+                         const spmv_plan *const *plans)
+{
+    *out = nullptr;
+    const Rccl *nc = rccl();
+    if (!nc) {
+        set_error("RCCL (librccl.so.1) could not be loaded");
+        return 1;
+    }
+    std::unique_ptr<spmv_mgpu> mg(new spmv_mgpu());
+    mg->nc = nc;
+    mg->init(n);
+    mg->owns_plans = false;
+    mg->own_x = false;
+    mg->nranks = n;
+    mg->bounds.assign(bounds, bounds + n + 1);
+    mg->nr_rows = bounds[n];
+    mg->nr_cols = nr_cols;
+    for (int d = 0; d < n; ++d) {
+        for (int e = 0; e < d; ++e)
+            if (devices[e] == devices[d]) {
+                set_error("a device appears twice (one RCCL rank per GPU)");
+                return 1;
+            }
+        mg->dev[d] = devices[d];
+        mg->rank[d] = d;
+        mg->plan[d] = plans[d];
+        if (mg->alloc_device(d))
+            return 1;
+    }
+    const ncclResult_t r = nc->CommInitAll(mg->comm.data(), n, devices);
+    if (r != ncclSuccess) {
+        mg->comm.assign(n, nullptr);
+        set_error(std::string("ncclCommInitAll: ") + nc->GetErrorString(r));
+        return 1;
+    }
+    *out = mg.release();
+    return 0;
+}
+
+const ValueType *mgpu_root_y(const spmv_mgpu *mg)
+{
+    const int r0 = mg->root_local();
+    return r0 < 0 ? nullptr : mg->y[r0];
+}
+
+// the SpMV on every local device with x_dev[d] (NULL: the handle's own x), then the exchange
+int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev)
+{
+    if (exchange < 0 || exchange > 2 || (!x_dev && !mg->own_x) || (exchange == 2 && !mg->own_x)) {
         set_error("spmv_mgpu_run: bad arguments");
         return 1;
     }
@@ -388,7 +470,7 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
     // buffers of the exchange form, allocated on first use
     for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
-        if (exchange == 1 && nr > 1 && !mg->ypart[d])
+        if (exchange == 1 && !mg->ypart[d])
             SPMV_TRY(hipMalloc((void **)&mg->ypart[d], std::max<size_t>(nb, sizeof(ValueType))));
         if (exchange == 2 && !mg->xnext[d])
             SPMV_TRY(hipMalloc((void **)&mg->xnext[d], std::max<size_t>(nb, sizeof(ValueType))));
@@ -398,7 +480,7 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
         const IndexType b = mg->bounds[mg->rank[d]];
         if (exchange == 2)
             return mg->xnext[d] + b;
-        if (exchange == 1 && nr > 1)
+        if (exchange == 1)
             return mg->ypart[d] + b;
         return mg->rank[d] == 0 ? mg->y[d] + b : mg->yslice[d];
     };
@@ -406,13 +488,14 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         hipStream_t s = mg->stream[d];
         SPMV_TRY(hipEventRecord(mg->ev[3 * d], s));
-        if (exchange == 1 && nr > 1)  // full-length partial: zero outside the slice
+        if (exchange == 1)  // full-length partial: zero outside the slice
             SPMV_TRY(hipMemsetAsync(mg->ypart[d], 0, nb, s));
-        if (mg->rows(d) && spmv_plan_run(mg->plan[d], mg->x[d], dst(d), s))
+        if (mg->rows(d) && spmv_plan_run(mg->plan[d], x_dev ? x_dev[d] : mg->x[d], dst(d), s))
             return 1;
         SPMV_TRY(hipEventRecord(mg->ev[3 * d + 1], s));
     }
-    if (nr > 1 && mg->nr_rows) {
+    // a reduce runs on one rank too (RCCL copies the partial into y): the same code path as N
+    if ((nr > 1 || exchange == 1) && mg->nr_rows) {
         MG_NCCL(mg->nc->GroupStart());
         for (int d = 0; d < nl; ++d) {
             hipStream_t s = mg->stream[d];
@@ -457,6 +540,19 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
         for (int d = 0; d < nl; ++d)
             std::swap(mg->x[d], mg->xnext[d]);  // y becomes the next x on every device
     return 0;
+}
+
+}  // namespace spmvhw
+
+extern "C" {
+
+int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
+{
+    if (!mg || exchange < 0 || exchange > 2 || !mg->own_x) {
+        set_error("spmv_mgpu_run: bad arguments");
+        return 1;
+    }
+    return mgpu_run_on(mg, exchange, nullptr);
 }
 
 // y (nr_rows values) to the host: rank 0's y after a gather / reduce, any rank's x after an

@@ -556,39 +556,44 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         return q;
     };
     if (kernel == kKernelTune) {
-        // build the tile, sweep, slice and binned layouts, time one SpMV of each on this matrix,
-        // keep the fastest
-        std::unique_ptr<spmv_plan> q = fresh(), r = fresh(), b = fresh();
-        r->slice_pad_limit = 2.0;  // a slice layout padded beyond 2x is built as tiles instead
-        if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s) ||
-            build_layout(*q, kKernelSweep, true, h_row_ptr, d_col, d_val, s) ||
-            build_layout(*r, kKernelSlices, true, h_row_ptr, d_col, d_val, s) ||
-            build_layout(*b, kKernelBinned, true, h_row_ptr, d_col, d_val, s))
-            return 1;
+        // build the tile, sweep, slice and binned layouts one at a time, time one SpMV of each on
+        // this matrix, keep the fastest: only the best so far and the candidate are resident, and
+        // a candidate whose build fails (e.g. out of memory) is dropped, not a plan error. The
+        // tiles are the fallback every matrix builds. With SPMV_SWEEP_DETERMINISTIC=1 the binned
+        // layout (pass-2 adds in timing order) is not a candidate: the switch promises fixed bits.
+        const char *det = std::getenv("SPMV_SWEEP_DETERMINISTIC");
+        const bool fixed_bits = det && det[0] == '1';
         Tmp tx, ty;
         SPMV_TRY(hipMalloc(&tx.p, std::max<size_t>(nr_cols, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMalloc(&ty.p, std::max<size_t>(nr_rows, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMemsetAsync(tx.p, 0, std::max<size_t>(nr_cols, 1) * sizeof(ValueType), s));
-        double mt = 1e30, ms = 1e30, ml = 1e30, mb = 1e30;
-        if (time_layout(*p, (const ValueType *)tx.p, (ValueType *)ty.p, s, &mt) ||
-            time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ms) ||
-            time_layout(*r, (const ValueType *)tx.p, (ValueType *)ty.p, s, &ml) ||
-            time_layout(*b, (const ValueType *)tx.p, (ValueType *)ty.p, s, &mb))
+        double tuned[4] = {1e30, 1e30, 1e30, 1e30};
+        if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s) ||
+            time_layout(*p, (const ValueType *)tx.p, (ValueType *)ty.p, s, &tuned[0]))
             return 1;
-        const double best = std::min({mt, ms, ml, mb});
-        if (mt == best)
-            ;  // ties keep the tiles
-        else if (ms == best)
-            p.swap(q);
-        else if (ml == best)
-            p.swap(r);
-        else if (mb == best)
-            p.swap(b);
-        p->tuned_ms[0] = mt;
-        p->tuned_ms[1] = ms;
-        p->tuned_ms[2] = ml;
-        p->tuned_ms[3] = mb;
-        trace("tune: build all + time", s);
+        double best = tuned[0];
+        const int cand[3] = {kKernelSweep, kKernelSlices, kKernelBinned};
+        for (int c = 0; c < 3; ++c) {
+            if (cand[c] == kKernelBinned && fixed_bits)
+                continue;
+            std::unique_ptr<spmv_plan> q = fresh();
+            if (cand[c] == kKernelSlices)
+                q->slice_pad_limit = 2.0;  // a slice layout padded beyond 2x is built as tiles instead
+            if (build_layout(*q, cand[c], true, h_row_ptr, d_col, d_val, s) ||
+                time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &tuned[c + 1])) {
+                tuned[c + 1] = 1e30;  // not a candidate
+                q.reset();
+                (void)hipGetLastError();
+                continue;
+            }
+            if (tuned[c + 1] < best) {  // ties keep the earlier layout (the tiles first)
+                best = tuned[c + 1];
+                p.swap(q);
+            }
+        }
+        for (int c = 0; c < 4; ++c)
+            p->tuned_ms[c] = tuned[c];
+        trace("tune: build + time each", s);
     } else if (requested_kernel() < 0 && kernel == kKernelTiles && nnz >= 65536) {
         // automatic, local columns: the slice layout when rows of a 64-row slice have about the
         // same length (<= 15 % padding) and every slot fits 16-bit (or clustered 16-bit) offsets
@@ -616,8 +621,15 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             trace("build tile layout", s);
         }
     } else {
-        if (kernel == kKernelBinned && requested_kernel() < 0)
+        if (kernel == kKernelBinned && requested_kernel() < 0) {
             p->bin_skew_limit = 2.0;  // automatic: skewed matrices stay on the sweep
+            // and so do matrices with a row above 0.3x a panel's mean entries: 2M x 6M fp32 with
+            // 64 rows of L (profiles/r03e_skew_rowlimit.jsonl; L / mean 0.12, 0.24, 0.44, 0.81):
+            // binned 0.136 / 0.178 / 0.254 / 0.282 ms, sweep 0.155 / 0.183 / 0.225 / 0.298
+            p->bin_row_limit = 0.3;
+            if (const char *e = std::getenv("SPMV_BIN_ROW_LIMIT"))
+                p->bin_row_limit = std::atof(e);
+        }
         if (build_layout(*p, kernel, requested_kernel() < 0, h_row_ptr, d_col, d_val, s))
             return 1;
         trace(p->kernel == kKernelSweep ? "build sweep layout" : p->kernel == kKernelBinned ? "build binned layout"

@@ -151,6 +151,9 @@ struct spmv_plan {
     double bin_skew_limit = 0.0;       // automatic choice: give up (rc 2) when a panel holds more than
                                        // this many times the mean entries (long rows: pass 2 would
                                        // serialise their LDS adds on one address)
+    double bin_row_limit = 0.0;        // automatic choice: give up (rc 2) when one row holds more than
+                                       // this fraction of a panel's mean entries (same reason; env
+                                       // SPMV_BIN_ROW_LIMIT overrides the automatic value)
     double locality = -1.0;    // probe result used by the automatic kernel choice
     double tuned_ms[4] = {-1.0, -1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: tiles / sweep / slices / binned ms
 
@@ -241,6 +244,14 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
                                  const IndexType *h_row_ptr /* rebased, nr_rows+1 */,
                                  const IndexType *col_src, const ValueType *val_src,
                                  bool src_on_device, hipStream_t s);
+
+// mgpu.cpp helpers for spmv_hw's RCCL merge (csr_hw_wrapper.cpp): a clique over n distinct
+// devices (one rank each, ncclCommInitAll) that borrows the units' plans and takes each device's
+// x per run; y of a gather / reduce lands in rank 0's full-length buffer
+int mgpu_create_borrowed(spmv_mgpu **out, int n, const int *devices, const IndexType *bounds, IndexType nr_cols,
+                         const spmv_plan *const *plans);
+int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev);
+const ValueType *mgpu_root_y(const spmv_mgpu *mg);
 }  // namespace spmvhw
 
 #define SPMV_TRY(expr)                                                                        \

@@ -104,7 +104,7 @@ EXPORTS = [
     "spmv_read_csr_header", "spmv_read_csr_matrix", "spmv_read_csr", "spmv_free_csr",
     "spmv_mgpu_create", "spmv_mgpu_set_x", "spmv_mgpu_run", "spmv_mgpu_get_y", "spmv_mgpu_get_timing",
     "spmv_mgpu_slice", "spmv_mgpu_destroy", "spmv_mgpu_unique_id", "spmv_mgpu_create_rank",
-    "spmv_mgpu_set_x_device", "spmv_mgpu_y_device",
+    "spmv_mgpu_set_x_device", "spmv_mgpu_set_x_device_on", "spmv_mgpu_y_device",
 ]
 
 MGPU_GATHER, MGPU_REDUCE, MGPU_ALLGATHER = 0, 1, 2  # include/csr_hw_wrapper.h SPMV_MGPU_*
@@ -177,6 +177,7 @@ class Lib:
             "spmv_mgpu_create_rank": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                                      ctypes.c_int, up, IndexType, vp]),
             "spmv_mgpu_set_x_device": (ctypes.c_int, [vp, vp]),
+            "spmv_mgpu_set_x_device_on": (ctypes.c_int, [vp, vp, vp]),
             "spmv_mgpu_y_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp)]),
         }
         for name, (res, args) in sig.items():
@@ -405,10 +406,16 @@ class MultiGpu:
         obj._plan = plan  # borrowed by the handle: keep it alive
         return obj
 
-    def set_x_device(self, x) -> None:
-        """Every rank calls it; x (a device tensor) is read on rank 0 only."""
-        self.lib._ok(self.lib.L.spmv_mgpu_set_x_device(self.h, ctypes.c_void_p(x.data_ptr() if x is not None else 0)),
-                     "spmv_mgpu_set_x_device")
+    def set_x_device(self, x, stream=None) -> None:
+        """Every rank calls it; x (a device tensor) is read on rank 0 only. The copy is ordered
+        after the torch stream that produced x (`stream`, default: the current stream) by an
+        event, with no host wait."""
+        if stream is None and x is not None:
+            import torch
+            stream = torch.cuda.current_stream(x.device)
+        sp = ctypes.c_void_p(stream.cuda_stream if stream is not None else 0)
+        self.lib._ok(self.lib.L.spmv_mgpu_set_x_device_on(self.h, ctypes.c_void_p(x.data_ptr() if x is not None else 0),
+                                                          sp), "spmv_mgpu_set_x_device_on")
 
     def y_device_ptr(self, exchange: int = MGPU_GATHER) -> int:
         p = ctypes.c_void_p()

@@ -137,3 +137,38 @@ def test_mgpu_rank_mode_rejects_a_foreign_plan():
     with pytest.raises(RuntimeError, match="not this rank's slice"):
         spmv_hw.MultiGpu.rank(lib, 0, 1, uid, 0, [0, n - 1], n, plan)
     plan.destroy()
+
+
+@pytest.mark.parametrize("form", ["on_stream", "whole_device"])
+def test_mgpu_set_x_device_waits_for_the_producer(form):
+    """x written on a side stream behind a long GPU sleep: the copy into the clique's x must wait
+    for it (the handle's streams are non-blocking). `on_stream` orders it after the
+    producer stream by an event, `whole_device` (the C call without a stream) after everything
+    queued on the device."""
+    import ctypes
+    import torch
+    lib = spmv_hw.load(np.float64)
+    n, z = 200_000, 3_200_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    mg = spmv_hw.MultiGpu.rank(lib, 0, 1, spmv_hw.mgpu_unique_id(lib), 0, [0, n], n, plan)
+    xs = torch.full_like(x, float("nan"))
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU time before x lands
+        xs.copy_(x)
+    if form == "on_stream":
+        mg.set_x_device(xs, stream=side)
+    else:
+        lib._ok(lib.L.spmv_mgpu_set_x_device(mg.h, ctypes.c_void_p(xs.data_ptr())), "spmv_mgpu_set_x_device")
+    mg.run(spmv_hw.MGPU_GATHER)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref = oracle.spmv_gold(r, c, h[2], h[3])
+    y = mg.y(spmv_hw.MGPU_GATHER)
+    assert np.isfinite(y).all()
+    assert oracle.scaled_error(r, c, h[2], h[3], ref, y) <= 1e-12
+    mg.destroy()
+    plan.destroy()

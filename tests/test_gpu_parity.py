@@ -939,6 +939,40 @@ def test_auto_binned_skips_skewed_fp32(torch, monkeypatch):
         assert oracle.scaled_error(row_ptr, c, v, xx, ref64, yy) <= 2e-6
 
 
+@pytest.mark.parametrize("ratio,limit,want", [(0.4, None, 2), (0.4, "1", 6), (0.15, None, 6)])
+def test_auto_binned_row_limit(torch, monkeypatch, ratio, limit, want):
+    """balanced panels let a row of up to ~2x the mean panel entries through the panel
+    test, and pass 2 adds all of it into one LDS address. The automatic choice also checks the
+    longest row against 0.3x the mean panel entries (profiles/r03e_skew_rowlimit.jsonl): a row of
+    0.4x keeps the sweep, 0.15x keeps the binned kernel; SPMV_BIN_ROW_LIMIT=1 lifts the row test
+    (the panel test still holds). y matches the oracle either way."""
+    monkeypatch.delenv("SPMV_HW_KERNEL", raising=False)
+    if limit:
+        monkeypatch.setenv("SPMV_BIN_ROW_LIMIT", limit)
+    else:
+        monkeypatch.delenv("SPMV_BIN_ROW_LIMIT", raising=False)
+    lib = spmv_hw.load(np.float32)
+    n, m, z = 2_000_000, 6_000_000, 32_000_000
+    panels = 256  # 2M rows: one round of the CUs, ~125K entries per panel
+    long_len = int(ratio * (z / panels))
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, z, seed=11)
+    dcol = torch.arange(0, 5 * long_len, 5, dtype=torch.int32, device="cuda")
+    rp = torch.cat([rp, (rp[-1:].long() + long_len).int()])
+    col = torch.cat([col[:z], dcol])
+    val = torch.cat([val[:z], torch.full((long_len,), 0.25, dtype=val.dtype, device="cuda")])
+    x = spmv_hw.gen_vector(lib, m, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, m)
+    assert plan.stats()["kernel"] == want
+    y = torch.full((n + 1,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    plan.destroy()
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref64 = oracle.spmv_fp64acc(row_ptr, c, v, xx)
+    assert oracle.scaled_error(row_ptr, c, v, xx, ref64, y.cpu().numpy()) <= 2e-6
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("points", [7, 27])
 def test_slices_stencil_narrow_equals_wide(torch, monkeypatch, dtype, points):

@@ -1,0 +1,120 @@
+"""spmv_hw (the reference's entry, csr_hw_wrapper.cpp:193-288) with the RCCL merge: when the units
+sit on distinct GPUs, the slices meet on GPU 0 over xGMI -- an RCCL gather of the disjoint slices
+(default) or, with SPMV_HW_MERGE=reduce, the literal ncclReduce(sum) of full-length partials
+(accum_results' `+=`, csr_hw.cpp:1531-1565) -- and one D2H copy brings y home. The box has one
+GPU, so these tests run the RCCL branch with one unit (forced by SPMV_HW_MERGE; a one-rank
+reduce still goes through RCCL); the driver's 8-GPU node takes the same code with 8. y is checked
+against the oracle's spmv_gold (csr.cpp:184-194) and the golden fixtures."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+import spmv_hw
+from conftest import DTYPES, FIXTURES, GOLDEN, golden_arrays, manifest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TIGHT = {np.dtype(np.float64): 1e-12, np.dtype(np.float32): 2e-6}
+
+
+def _ndev():
+    import torch
+    return torch.cuda.device_count()
+
+
+def _flow(lib, row_ptr, col, val, x, ncols, dtype, calls=1):
+    m = lib.make_csr_matrix(row_ptr, col, val, ncols)
+    hw, bm = lib.create_csr_hw_matrix(m)
+    hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(x), 1, hw[0].contents.nr_cols)
+    r = len(row_ptr) - 1
+    yv = lib.make_csr_vector(np.zeros(r, dtype))
+    ys = []
+    for _ in range(calls):
+        lib.spmv_hw(hw, hx, yv, bm)
+        ys.append(np.ctypeslib.as_array(yv.values, shape=(r,)).copy())
+    lib.delete_csr_hw_matrix(hw)
+    lib.free_bitmap(bm)
+    lib.delete_csr_hw_x_vector(hx)
+    return ys
+
+
+@pytest.mark.parametrize("merge", ["gather", "reduce"])
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("dtype,tag", DTYPES)
+def test_rccl_merge_on_golden_fixtures(monkeypatch, capfd, merge, name, dtype, tag):
+    monkeypatch.setenv("SPMV_NGPUS", str(_ndev()))
+    monkeypatch.setenv("SPMV_HW_MERGE", merge)
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    lib = spmv_hw.load(dtype)
+    _, c, row_ptr, col, val, _ = oracle.read_csr(os.path.join(GOLDEN, manifest()[name]["file"]), dtype)
+    x, y_gold = golden_arrays(name, tag)
+    y1, y2 = _flow(lib, row_ptr, col, val, x, c, dtype, calls=2)
+    tol = TIGHT[np.dtype(dtype)]
+    assert oracle.scaled_error(row_ptr, col, val, x, y_gold, y1) <= tol
+    # spmv_hw accumulates (+=): the second call adds another A*x
+    second = y2.astype(np.float64) - y1.astype(np.float64)
+    assert oracle.scaled_error(row_ptr, col, val, x, y1.astype(np.float64), second) <= (1e-5 if dtype == np.float32 else 1e-12)
+    out, err = capfd.readouterr()
+    # the reference's three lines (csr_hw_wrapper.cpp:274,284-285), once per call
+    assert out.count("Hardware execution time : ") == 2
+    assert out.count("Result accumulation time : ") == 2
+    assert out.count("Total time  : ") == 2
+    assert "RCCL merge" in err  # the trace names the branch that ran
+
+
+@pytest.mark.parametrize("merge", ["gather", "reduce", "host"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_rccl_merge_powerlaw(monkeypatch, capfd, merge, dtype):
+    """A 1M-row power-law matrix (sweep / binned plans) through each merge; host is the PCIe
+    merge the RCCL branch replaces."""
+    monkeypatch.setenv("SPMV_NGPUS", str(_ndev()))
+    monkeypatch.setenv("SPMV_HW_MERGE", merge)
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    lib = spmv_hw.load(dtype)
+    n, z = 1_000_000, 16_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    h_rp, h_col = rp.cpu().numpy().view(np.uint32), col.cpu().numpy().view(np.uint32)
+    h_val, h_x = val.cpu().numpy(), x.cpu().numpy()
+    (y,) = _flow(lib, h_rp, h_col, h_val, h_x, n, dtype)
+    ref = oracle.spmv_fp64acc(h_rp, h_col, h_val, h_x) if dtype == np.float32 else oracle.spmv_gold(h_rp, h_col, h_val, h_x)
+    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y) <= TIGHT[np.dtype(dtype)]
+    _, err = capfd.readouterr()
+    assert ("RCCL merge" in err) == (merge != "host")
+
+
+def test_rccl_merge_refuses_shared_gpus():
+    """SPMV_HW_MERGE=gather asks for one RCCL rank per unit: more units than GPUs fails fast
+    (the Part-1 error behaviour: a message and exit(1)), in a child process."""
+    code = (
+        "import sys, numpy as np; sys.path[:0] = [%r, %r]\n"
+        "import spmv_hw\n"
+        "lib = spmv_hw.load(np.float64)\n"
+        "rp = np.array([0, 1, 2], np.uint32)\n"
+        "m = lib.make_csr_matrix(rp, np.array([0, 1], np.uint32), np.ones(2), 2)\n"
+        "lib.create_csr_hw_matrix(m)\n"
+    ) % (os.path.join(ROOT, "spmv-fpga_amd"), os.path.join(ROOT, "oracle"))
+    env = dict(os.environ, SPMV_NGPUS=str(_ndev() + 1), SPMV_HW_MERGE="gather")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1
+    assert "needs one unit per GPU" in p.stderr
+
+
+def test_auto_merge_keeps_host_for_shared_gpus(monkeypatch, capfd):
+    """Automatic choice: 3 virtual units on the box's one GPU cannot form an RCCL clique, so the
+    per-unit PCIe merge runs (and gives the oracle's y)."""
+    monkeypatch.setenv("SPMV_NGPUS", str(_ndev() + 2))
+    monkeypatch.delenv("SPMV_HW_MERGE", raising=False)
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    lib = spmv_hw.load(np.float64)
+    _, c, row_ptr, col, val, _ = oracle.read_csr(os.path.join(GOLDEN, manifest()["small"]["file"]), np.float64)
+    x, y_gold = golden_arrays("small", "f64")
+    (y,) = _flow(lib, row_ptr, col, val, x, c, np.float64)
+    assert oracle.scaled_error(row_ptr, col, val, x, y_gold, y) <= 1e-12
+    _, err = capfd.readouterr()
+    assert "RCCL merge" not in err
