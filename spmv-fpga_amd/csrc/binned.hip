@@ -78,21 +78,6 @@ template <int PER> struct BinDelta;
 template <> struct BinDelta<4> { typedef uint32_t T; };
 template <> struct BinDelta<2> { typedef uint16_t T; };
 
-// 64-lane inclusive prefix sum (the GCN DPP sequence: row_shr 1/2/3 of the source, row_shr 4/8
-// with bank masks, row_bcast 15/31 with row masks); tools/delta_probe.hip checks it
-__device__ __forceinline__ uint32_t bin_wave_inclusive_sum(uint32_t v0)
-{
-    uint32_t v = v0;
-    v += __builtin_amdgcn_update_dpp(0u, v0, 0x111, 0xf, 0xf, true);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0u, v0, 0x112, 0xf, 0xf, true);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0u, v0, 0x113, 0xf, 0xf, true);  // row_shr:3
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xe, true);   // row_shr:4, banks 1-3
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xc, true);   // row_shr:8, banks 2-3
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15, rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31, rows 2, 3
-    return v;
-}
-
 // Pass 1: unit u = entries [ub[u], ub[u+1]) of window uwin[u] (both multiples of PER).
 // AL: x is 16-byte aligned, so the window is staged with 16-byte loads.
 template <typename V, bool AL>
@@ -185,7 +170,10 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
 // DELTA: `rowp` holds 1-byte row deltas (segments sorted by row, each starting from row 0); a
 // step's rows are its deltas' running sum: a 64-lane prefix sum of the lanes' PER-delta totals
 // plus the carry of the segment's earlier steps.
-template <typename V, bool DELTA>
+// ABL (measurement-only ablations, tools library; wrong y): 1 = no LDS adds (products summed into
+// a register, added once at the end: the memory stream alone), 2 = loads re-read the wave's first
+// 16 steps (L2-resident: the LDS adds and decode alone)
+template <typename V, bool DELTA, int ABL = 0>
 __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, const void *__restrict__ rowp,
                                                    const uint64_t *__restrict__ seg,
                                                    const uint32_t *__restrict__ panel_row, uint32_t nwin,
@@ -238,6 +226,7 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
     const uint16_t *__restrict__ rows16 = reinterpret_cast<const uint16_t *>(rowp);
     const uint8_t *__restrict__ rows8 = reinterpret_cast<const uint8_t *>(rowp);
     uint32_t carry = 0;  // DELTA: row of the segment's last entry so far
+    double sink = 0.0;   // ABL 1 only
     while (o < nmine) {
         VT v[kBinD];
         IT r[kBinD];
@@ -260,11 +249,14 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
             en[k] = o < nmine ? end : 0;
             fresh[k] = moved;
             if (at[k] < en[k]) {
-                v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + at[k]));
+                uint64_t ld = at[k];
+                if constexpr (ABL == 2)
+                    ld = (ld & ~(uint64_t)(16 * STEP - 1)) == 0 ? ld : (ld & (16 * STEP - 1));
+                v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + ld));
                 if (DELTA)
-                    dl[k] = __builtin_nontemporal_load(reinterpret_cast<const DT *>(rows8 + at[k]));
+                    dl[k] = __builtin_nontemporal_load(reinterpret_cast<const DT *>(rows8 + ld));
                 else
-                    r[k] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(rows16 + at[k]));
+                    r[k] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(rows16 + ld));
             } else {
                 dl[k] = 0;
             }
@@ -281,7 +273,7 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
                     d[q] = ((uint32_t)dl[k] >> (8 * q)) & 0xFFu;
                     t += d[q];
                 }
-                const uint32_t inc = bin_wave_inclusive_sum(t);
+                const uint32_t inc = wave_inclusive_sum(t);
                 uint32_t row = carry + inc - t;
                 carry += (uint32_t)__builtin_amdgcn_readlane(inc, 63);
 #pragma unroll
@@ -291,12 +283,20 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
                 }
             }
             if (at[k] < en[k]) {
+                if constexpr (ABL == 1) {
 #pragma unroll
-                for (int q = 0; q < PER; ++q)
-                    atomicAdd(&ys[r[k][q]], (double)v[k][q]);
+                    for (int q = 0; q < PER; ++q)
+                        sink += (double)v[k][q] * (double)(r[k][q] + 1);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < PER; ++q)
+                        atomicAdd(&ys[r[k][q]], (double)v[k][q]);
+                }
             }
         }
     }
+    if constexpr (ABL == 1)
+        atomicAdd(&ys[0], sink);
     __syncthreads();
     const uint32_t r0 = panel_row[p], nr = panel_row[p + 1] - r0;
     for (uint32_t i = threadIdx.x; i < nr; i += kBinT)
@@ -464,6 +464,17 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
         reinterpret_cast<uintptr_t>(p.d_b_prod) - base * sizeof(ValueType));
     const void *rowp = reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(p.d_b_rowp) -
                                                       base * (p.b_delta ? 1 : 2));
+#ifdef SPMV_ABLATIONS
+    if (p.b_delta && (p.variant == 51 || p.variant == 52)) {
+        if (p.variant == 51)
+            launch_or_warm(warm, k_bin_acc<ValueType, true, 1>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod,
+                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
+        else
+            launch_or_warm(warm, k_bin_acc<ValueType, true, 2>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod,
+                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
+        return hipGetLastError();
+    }
+#endif
     if (p.b_delta)
         launch_or_warm(warm, k_bin_acc<ValueType, true>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod, rowp,
                        seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);

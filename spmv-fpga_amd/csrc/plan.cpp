@@ -651,7 +651,7 @@ spmv_plan::~spmv_plan()
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
                       (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
-                      (void *)d_s_cbase, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
+                      (void *)d_s_cbase, (void *)d_s_row16, (void *)d_s_d8, (void *)d_s_dbase, (void *)d_s_side, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
                       (void *)d_sbase, (void *)d_slice_len, (void *)d_b_val, (void *)d_b_colw, (void *)d_b_rowp,
                       (void *)d_b_prod, (void *)d_b_seg, (void *)d_b_seg_hi, (void *)d_b_ub, (void *)d_b_uwin})
@@ -683,7 +683,8 @@ uint64_t spmv_plan::device_bytes() const
         return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
                (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * sweep_acc_bytes : 0) + nunits * 4 + (npanels + 1) * 4 +
-               (d_panel_cnt ? npanels * 4 : 0);
+               (d_panel_cnt ? npanels * 4 : 0) +
+               (sweep_delta ? ent_pad * 3 + ent_pad / kSweepChunk * 4 + sweep_side_chunks * kSweepChunk * 4 : 0);
     return nnz_pad * (tile_col_bytes + sizeof(ValueType)) + nnz_pad / 8 + (ntiles + 1) * 4 +
            (tile_col_bytes < 4 ? ntiles * (tile_clustered ? 16 : 4) : 0) +
            (has_empty ? nzr * 4 : 0) + ntiles * 2 * sizeof(ValueType) + ncross * 12;
@@ -877,7 +878,7 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->kernel = p->kernel;
     st->blocks = p->kernel == kKernelBlocked ? (uint32_t)((uint64_t(p->nr_cols) + p->fpga_width - 1) / p->fpga_width) : 1;
     st->format = (p->kernel == kKernelSlices && p->slice_off_bytes < 4 ? 1 : 0) | (p->slice_clustered ? 16 : 0) |
-                 (p->kernel == kKernelSlices && p->slice_off_bytes == 1 ? 8 : 0) | (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) |
+                 (p->kernel == kKernelSlices && p->slice_off_bytes == 1 ? 8 : 0) | (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) | (p->sweep_delta ? 64 : 0) |
                  (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0) |
                  (p->kernel == kKernelBinned && p->b_delta ? 32 : 0);
     return 0;
@@ -892,7 +893,8 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
 #ifndef SPMV_ABLATIONS
     // the measurement-only ablations (some give a wrong y by design) exist only in the tools
     // library built with -DSPMV_ABLATIONS (Makefile target `ablations`, tools/ab_variants.py)
-    if ((p->kernel == kKernelSweep && variant >= 51 && variant <= 63) || (p->kernel == kKernelBlocked && variant == 1)) {
+    if ((p->kernel == kKernelSweep && variant >= 50 && variant <= 63) || (p->kernel == kKernelBlocked && variant == 1) ||
+        (p->kernel == kKernelBinned && variant >= 51 && variant <= 52)) {
         set_error("spmv_plan_set_variant: measurement-only ablation variant (tools library only)");
         return 1;
     }
@@ -903,7 +905,8 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
         // 1 / 2 (tests, same y): pass 2 reads segment offsets rebased so that they straddle 2^31 /
         // 2^32 entries (prod and rowp rebased the other way: the same addresses), which drives the
         // 64-bit bound widening after readlane (binned.hip, k_bin_acc) without a 2^31-entry matrix
-        if (variant > 2) {
+        // 51 / 52 (tools library): pass-2 ablations, binned.hip
+        if (variant > 2 && !(variant >= 51 && variant <= 52)) {
             set_error("spmv_plan_set_variant: binned variants are 0, 1 and 2");
             return 1;
         }
@@ -913,7 +916,7 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
             p->d_b_seg_hi = nullptr;
             p->b_seg_base = 0;
         }
-        if (variant) {
+        if (variant == 1 || variant == 2) {
             SPMV_TRY(hipSetDevice(p->device));
             const uint64_t nseg = uint64_t(p->b_nwin) * p->npanels + 1;
             std::vector<uint64_t> h(nseg);

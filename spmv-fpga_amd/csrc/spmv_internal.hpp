@@ -55,6 +55,22 @@ constexpr int kKernelBinned = 6;   // two passes: products per column window, su
                                    // (propagation blocking, binned.hip)
 constexpr int kGoldLong = 128;   // gold plan stats: rows longer than this count as long
 
+// 64-lane inclusive prefix sum (the GCN DPP sequence: row_shr 1/2/3 of the source, row_shr 4/8
+// with bank masks, row_bcast 15/31 with row masks); tools/delta_probe.hip checks it. Used by the
+// binned kernel's row deltas and the sweep's column deltas.
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v0)
+{
+    uint32_t v = v0;
+    v += __builtin_amdgcn_update_dpp(0u, v0, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v0, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v0, 0x113, 0xf, 0xf, true);  // row_shr:3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xe, true);   // row_shr:4, banks 1-3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xc, true);   // row_shr:8, banks 2-3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15, rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31, rows 2, 3
+    return v;
+}
+
 }  // namespace spmvhw
 
 struct spmv_plan {
@@ -134,6 +150,16 @@ struct spmv_plan {
     bool sweep_packed = false;
     bool sweep_lane_order = false;   // packed chunks stored in lane order (k_sweep_lane_order)
     bool sweep_det = false;          // env SPMV_SWEEP_DETERMINISTIC=1: ordered LDS adds (k_spmv_sweep_turn)
+    // delta-coded columns (default for packed lane-ordered plans, env SPMV_SWEEP_DELTA=0 off): the
+    // default kernel streams 11 B/entry fp64 (7 fp32) instead of 12 (8); the 12-byte rc words
+    // stay resident for the kernels that read them (deterministic variants, ablations)
+    uint16_t *d_s_row16 = nullptr;   // row in panel per entry (bits 0-14) + bit 8 of its delta (lane order)
+    uint8_t *d_s_d8 = nullptr;       // low 8 bits of the column minus the previous entry's column of
+                                     // the same wave instruction (the first from the chunk base)
+    uint32_t *d_s_dbase = nullptr;   // per chunk: base column, or bit 31 | index into d_s_side
+    uint32_t *d_s_side = nullptr;    // absolute columns (lane order) of chunks with a gap > 511
+    uint64_t sweep_side_chunks = 0;
+    bool sweep_delta = false;
     // binned representation (kernel 6, binned.hip): reuses npanels, panel_rmax, d_panel_row and
     // ent_pad of the sweep fields; entries ordered (window, panel), segments padded
     uint32_t b_nwin = 0, b_W = 0;      // column windows of b_W columns (x staged in LDS by pass 1)

@@ -279,15 +279,23 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
 // LAG = 0: one workgroup barrier per iteration. LAG = k > 0: no barrier; each wave publishes
 // its iteration count in LDS and only waits (s_sleep) while it is more than k iterations
 // ahead of the slowest wave, so the vector-memory pipe never drains at a common barrier.
-template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double>
+// DL: delta-coded columns (11 B/entry fp64, 7 fp32): per entry a u16 row word and a u8, which
+// together hold the row (15 bits) and a 9-bit column delta from the previous entry of the same
+// wave instruction; a chunk's first entry counts from the chunk base dbase[c]. A 64-lane DPP
+// prefix sum turns the deltas into columns. A chunk with a gap above 511 (~1 in 10^5 on the
+// headline matrix) has bit 31 of dbase set and its absolute columns in `side` (uniform branch).
+template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double, bool DL = false>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
     A *__restrict__ part, uint32_t stride, uint32_t *__restrict__ pcnt, const V *__restrict__ x,
-    V *__restrict__ y)
+    V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
+    const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+    typedef uint8_t u8x2 __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     A *ylds = reinterpret_cast<A *>(smem);
     const uint32_t p = unit_panel[blockIdx.x];  // unit = a piece of a panel's column-sorted entries
@@ -313,6 +321,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         uint32_t cb[Q];
         V v[Q][2];
         bool ok[Q];
+        u16x2 r16[Q];  // DL only
+        u8x2 dd[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             uint64_t wbase = base + q * kGroup + 128ull * wave;  // this wave's chunk
@@ -321,7 +331,38 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
             if constexpr (ABL == 3 || ABL == 4 || ABL == 9)  // ablation: entries re-read from the unit's first 4K (L2-resident)
                 wbase = e0 + ((wbase - e0) & 4095u);
             const uint64_t e = wbase + lane2;
-            w[q] = lds_<NT>(reinterpret_cast<const u32x2 *>(rc + e));
+            if constexpr (DL) {
+                r16[q] = lds_<NT>(reinterpret_cast<const u16x2 *>(row16 + e));
+                dd[q] = lds_<NT>(reinterpret_cast<const u8x2 *>(d8 + e));
+                cb[q] = dbase[wbase >> 7];
+                loadv<NT, 2>(val, e, v[q]);
+                continue;
+            }
+            if constexpr (ABL == 11) {
+                // ablation (wrong y): an 11-byte entry stream -- u16 row + u8 column delta per
+                // entry from two regions of the rc array (2 + 1 B instead of 4), columns decoded by
+                // a 64-lane prefix sum of the deltas (the cost of delta-coded columns)
+                typedef uint16_t u16x2_t __attribute__((ext_vector_type(2)));
+                typedef uint8_t u8x2_t __attribute__((ext_vector_type(2)));
+                const u16x2_t r16 = lds_<NT>(reinterpret_cast<const u16x2_t *>(reinterpret_cast<const uint16_t *>(rc) + e));
+                const u8x2_t d8 = lds_<NT>(reinterpret_cast<const u8x2_t *>(
+                    reinterpret_cast<const uint8_t *>(rc) + 2 * (uint64_t)unit_ent[gridDim.x] + e));
+                const uint32_t dsum = (uint32_t)(d8.x & 63u) + (uint32_t)(d8.y & 63u);
+                // 64-lane inclusive prefix sum by DPP (the binned kernel's row-delta decode)
+                uint32_t inc = dsum;
+                inc += __builtin_amdgcn_update_dpp(0u, dsum, 0x111, 0xf, 0xf, true);
+                inc += __builtin_amdgcn_update_dpp(0u, dsum, 0x112, 0xf, 0xf, true);
+                inc += __builtin_amdgcn_update_dpp(0u, dsum, 0x113, 0xf, 0xf, true);
+                inc += __builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xf, 0xe, true);
+                inc += __builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xf, 0xc, true);
+                inc += __builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xa, 0xf, false);
+                inc += __builtin_amdgcn_update_dpp(0u, inc, 0x143, 0xc, 0xf, false);
+                const uint32_t c0 = inc - dsum + (d8.x & 63u);
+                w[q].x = ((uint32_t)(r16.x & 16383u) << 16) | (c0 & 0xFFFFu);
+                w[q].y = ((uint32_t)(r16.y & 16383u) << 16) | ((c0 + (d8.y & 63u)) & 0xFFFFu);
+            } else {
+                w[q] = lds_<NT>(reinterpret_cast<const u32x2 *>(rc + e));
+            }
             cb[q] = cbase[wbase >> 7];
             if constexpr (ABL == 10) {  // ablation: one value per two entries (8 B/entry streamed, not 12)
                 v[q][0] = v[q][1] = lds_<NT>(val + (wbase >> 1) + (lane2 >> 1));
@@ -334,7 +375,26 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         for (int q = 0; q < Q; ++q) {
             // ABL (measurement-only ablations, variants 60/61): 1 = x index folded into a 256 KiB
             // window (every gather an L2 hit, same request count), 2 = no gathers
-            if constexpr (ABL == 2 || ABL == 5) {
+            if constexpr (DL) {
+                // per group: its columns, then its two gathers (decoding every group's columns
+                // before any gather measured 3 % slower, profiles/r03_delta_columns.jsonl)
+                uint32_t cx, cy;
+                if (cb[q] & 0x80000000u) {  // wave-uniform: a chunk with a gap > 511
+                    const uint64_t sb = (uint64_t)(cb[q] & 0x7FFFFFFFu) * kSweepChunk + lane2;
+                    const u32x2 cc = lds_<NT>(reinterpret_cast<const u32x2 *>(side + sb));
+                    cx = cc.x;
+                    cy = cc.y;
+                } else {
+                    // 9-bit deltas: bit 15 of the row word is the delta's bit 8 (rows < 32768)
+                    const uint32_t dx = dd[q].x | ((uint32_t)(r16[q].x >> 15) << 8);
+                    const uint32_t dy = dd[q].y | ((uint32_t)(r16[q].y >> 15) << 8);
+                    const uint32_t i0 = wave_inclusive_sum(dx), i1 = wave_inclusive_sum(dy);
+                    cx = cb[q] + i0;
+                    cy = cb[q] + (uint32_t)__builtin_amdgcn_readlane(i0, 63) + i1;
+                }
+                xv[q][0] = x[cx];
+                xv[q][1] = x[cy];
+            } else if constexpr (ABL == 2 || ABL == 5) {
                 xv[q][0] = V(w[q].x & 1u);
                 xv[q][1] = V(w[q].y & 1u);
             } else if constexpr (ABL == 6) {  // x gathers non-temporal (nt)
@@ -358,8 +418,13 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
             A pv[2 * Q];
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
-                ri[2 * q] = ok[q] ? (w[q].x >> 16) : R;
-                ri[2 * q + 1] = ok[q] ? (w[q].y >> 16) : R;
+                if constexpr (DL) {
+                    ri[2 * q] = ok[q] ? (uint32_t)(r16[q].x & 0x7FFFu) : R;
+                    ri[2 * q + 1] = ok[q] ? (uint32_t)(r16[q].y & 0x7FFFu) : R;
+                } else {
+                    ri[2 * q] = ok[q] ? (w[q].x >> 16) : R;
+                    ri[2 * q + 1] = ok[q] ? (w[q].y >> 16) : R;
+                }
                 pv[2 * q] = A(v[q][0]) * A(xv[q][0]);
                 pv[2 * q + 1] = A(v[q][1]) * A(xv[q][1]);
             }
@@ -619,6 +684,77 @@ __global__ void k_sweep_lane_order(const uint32_t *__restrict__ rc_in, const V *
     v_out[m] = v_in[k];
 }
 
+// Delta-coded columns of a lane-ordered packed chunk (one thread per chunk). The chunk's entries
+// are first put in ascending column order (the radix sort keys drop the low `shift` column bits
+// for large matrices, so entries of one bucket keep their CSR order; rc words and values move
+// together, in place). Then per entry: the column minus the previous column of the same wave
+// instruction (the first of instruction 0 from the chunk base; instruction 1 continues from entry
+// 63) as 9 bits -- the low 8 in d8, bit 8 in bit 15 of the row word (panel rows < 32768) -- and
+// the row, in lane order; flag = some gap > 511 (the chunk's columns go to the side table).
+template <typename V>
+__global__ void k_sweep_delta(uint32_t *__restrict__ rc, V *__restrict__ val, uint64_t nchunks,
+                              uint16_t *__restrict__ row16, uint8_t *__restrict__ d8, uint8_t *__restrict__ flag)
+{
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks)
+        return;
+    constexpr int G = (int)kSweepChunk;
+    uint32_t w[G];
+    V v[G];
+    uint32_t *cw = rc + c * G;
+    V *cv = val + c * G;
+    for (int k = 0; k < G; ++k) {  // logical entry k sits at word 2 (k mod 64) + k / 64
+        const int m = 2 * (k & 63) + (k >> 6);
+        w[k] = cw[m];
+        v[k] = cv[m];
+    }
+    for (int k = 1; k < G; ++k) {  // stable insertion sort by column offset (nearly sorted input)
+        const uint32_t wk = w[k];
+        const V vk = v[k];
+        int j = k - 1;
+        while (j >= 0 && (w[j] & 0xFFFFu) > (wk & 0xFFFFu)) {
+            w[j + 1] = w[j];
+            v[j + 1] = v[j];
+            --j;
+        }
+        w[j + 1] = wk;
+        v[j + 1] = vk;
+    }
+    uint32_t prev = 0;
+    bool big = false;
+    for (int k = 0; k < G; ++k) {
+        const int m = 2 * (k & 63) + (k >> 6);
+        const uint32_t off = w[k] & 0xFFFFu;
+        const uint32_t d = off - prev;
+        big |= d > 511u;
+        cw[m] = w[k];
+        cv[m] = v[k];
+        row16[c * G + m] = (uint16_t)((w[k] >> 16) | ((d >> 8) & 1u) << 15);
+        d8[c * G + m] = (uint8_t)d;
+        prev = off;
+    }
+    flag[c] = big ? 1 : 0;
+}
+
+// per chunk: dbase = the chunk base, or bit 31 | its side-table index (sidx[c] != ~0), whose 128
+// absolute columns are written in lane order
+__global__ void k_sweep_delta_base(const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase,
+                                   const uint32_t *__restrict__ sidx, uint64_t nchunks, uint32_t *__restrict__ dbase,
+                                   uint32_t *__restrict__ side)
+{
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks)
+        return;
+    const uint32_t k = sidx[c];
+    if (k == 0xFFFFFFFFu) {
+        dbase[c] = cbase[c];
+        return;
+    }
+    dbase[c] = 0x80000000u | k;
+    for (uint64_t m = 0; m < kSweepChunk; ++m)
+        side[(uint64_t)k * kSweepChunk + m] = cbase[c] + (rc[c * kSweepChunk + m] & 0xFFFFu);
+}
+
 // sort key of every entry: (panel, column bucket); one thread per row
 __global__ void k_sweep_keys(const IndexType *__restrict__ rp, const IndexType *__restrict__ col,
                              const uint32_t *__restrict__ panel_row, uint32_t npanels, IndexType nrows,
@@ -762,7 +898,13 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     if (p.sweep_packed) {
 #define PKN(NT, Q, LAG, ABL)                                                                        \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
-                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y)
+                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
+                       (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr)
+    // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
+#define PKD()                                                                                         \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true>, grid, block, lds, s, p.d_s_col, \
+                       p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
+                       p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
@@ -792,9 +934,18 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 57: PKA(6); break;  // x gathers with the nt bit
         case 58: PKA(7); break;  // x gathers that bypass L1 (sc1)
         case 53: PKA(10); break;  // half the value bytes: 8 B/entry streamed instead of 12
+        case 50: if (p.panel_rmax >= 16384) { PKA(11); } else { PK(2, 2); } break;  // 11-B entries + delta decode
 #endif
-        default: PK(2, 2); break;
+        case 35: PK(2, 2); break;  // variant 28 on the 12-byte rc words of a delta plan (A/B)
+        default:
+            if (p.sweep_delta) {
+                PKD();
+            } else {
+                PK(2, 2);
+            }
+            break;
         }
+#undef PKD
 #undef PKA
 #undef PK
 #undef PKN
@@ -1092,6 +1243,47 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                 p.d_s_col = rc2;
                 p.d_s_val = v2;
                 p.sweep_lane_order = true;
+                // delta-coded columns for the default kernel (env SPMV_SWEEP_DELTA=0 keeps the
+                // 12-byte words only). The deterministic form reads the rc words, so it skips them
+                const char *de = std::getenv("SPMV_SWEEP_DELTA");
+                if (!(de && de[0] == '0') && !det && nchunks && uint64_t(p.nr_cols) < (1ull << 31) &&
+                    rmax_used < 32768) {
+                    uint8_t *d_flag = nullptr;
+                    uint32_t *d_sidx = nullptr;
+                    SW_TRY(hipMalloc((void **)&p.d_s_row16, p.ent_pad * 2));
+                    SW_TRY(hipMalloc((void **)&p.d_s_d8, p.ent_pad));
+                    SW_TRY(hipMalloc((void **)&p.d_s_dbase, nchunks * 4));
+                    SW_TRY(hipMalloc((void **)&d_flag, nchunks));
+                    hipLaunchKernelGGL((k_sweep_delta<ValueType>), dim3((unsigned)((nchunks + 63) / 64)), dim3(64), 0, s,
+                                       p.d_s_col, p.d_s_val, nchunks, p.d_s_row16, p.d_s_d8, d_flag);
+                    hipError_t e = hipGetLastError();
+                    std::vector<uint8_t> hf(nchunks);
+                    if (e == hipSuccess)
+                        e = hipMemcpyAsync(hf.data(), d_flag, nchunks, hipMemcpyDeviceToHost, s);
+                    if (e == hipSuccess)
+                        e = hipStreamSynchronize(s);
+                    (void)hipFree(d_flag);
+                    SW_TRY(e);
+                    std::vector<uint32_t> sidx(nchunks, 0xFFFFFFFFu);
+                    uint64_t ns = 0;
+                    for (uint64_t c = 0; c < nchunks; ++c)
+                        if (hf[c])
+                            sidx[c] = (uint32_t)ns++;
+                    p.sweep_side_chunks = ns;
+                    SW_TRY(hipMalloc((void **)&p.d_s_side, std::max<uint64_t>(ns, 1) * kSweepChunk * 4));
+                    SW_TRY(hipMalloc((void **)&d_sidx, nchunks * 4));
+                    e = hipMemcpyAsync(d_sidx, sidx.data(), nchunks * 4, hipMemcpyHostToDevice, s);
+                    if (e == hipSuccess) {
+                        hipLaunchKernelGGL(k_sweep_delta_base, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s,
+                                           p.d_s_col, p.d_s_cbase, d_sidx, nchunks, p.d_s_dbase, p.d_s_side);
+                        e = hipGetLastError();
+                    }
+                    if (e == hipSuccess)
+                        e = hipStreamSynchronize(s);
+                    (void)hipFree(d_sidx);
+                    SW_TRY(e);
+                    p.sweep_delta = true;
+                }
             }
         } else {
             SW_TRY(hipFree(p.d_s_cbase));

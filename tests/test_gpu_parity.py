@@ -28,9 +28,9 @@ def torch():
     return t
 
 
-KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "blocked", "slices", "slices_wide",
+KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_rc", "sweep_unpacked", "sweep_det", "gold", "blocked", "slices", "slices_wide",
            "binned", "binned_delta", "binned_u16"]
-KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_unpacked": 2, "sweep_det": 2, "gold": 1, "blocked": 4,
+KERNEL_ID = {"tiles": 0, "tiles_wide": 0, "sweep": 2, "sweep_rc": 2, "sweep_unpacked": 2, "sweep_det": 2, "gold": 1, "blocked": 4,
              "slices": 5, "slices_wide": 5, "binned": 6, "binned_delta": 6, "binned_u16": 6}
 
 
@@ -39,7 +39,8 @@ def kernel(request, monkeypatch):
     """Plans are built with SPMV_HW_KERNEL forced to each kernel in turn ("blocked" with its
     defaults VF = 1, 32768-column blocks); "tiles_wide" is the
     tile kernel with 32-bit columns (SPMV_TILE_NARROW=0) instead of per-tile offsets and
-    "sweep_unpacked" the sweep on 14-byte entries (SPMV_SWEEP_PACKED=0), the layout used when a
+    "sweep_rc" the packed sweep on its 12-byte words without delta-coded columns
+    (SPMV_SWEEP_DELTA=0); "sweep_unpacked" the sweep on 14-byte entries (SPMV_SWEEP_PACKED=0), the layout used when a
     chunk of a panel spans >= 65536 columns; "sweep_det" the deterministic sweep
     (SPMV_SWEEP_DETERMINISTIC=1); "slices_wide" the slice kernel with 32-bit columns
     (SPMV_SLICE_NARROW=0); "binned" the two-pass propagation-blocking kernel (binned.hip) with its
@@ -50,6 +51,8 @@ def kernel(request, monkeypatch):
         monkeypatch.setenv("SPMV_TILE_NARROW", "0")
     if request.param == "sweep_unpacked":
         monkeypatch.setenv("SPMV_SWEEP_PACKED", "0")
+    if request.param == "sweep_rc":  # packed 12-byte words without the delta-coded columns
+        monkeypatch.setenv("SPMV_SWEEP_DELTA", "0")
     if request.param == "sweep_det":  # deterministic sweep: LDS adds in a fixed (iteration, wave) order
         monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
     if request.param == "slices_wide":
@@ -84,6 +87,8 @@ def run_device(torch, lib, row_ptr, col, val, x, nr_cols, poison=True, expect_ke
             assert not stats["format"] & 1
         if expect_kernel == "sweep_unpacked":
             assert not stats["format"] & 2
+        if expect_kernel == "sweep_rc":
+            assert not stats["format"] & 64
         if expect_kernel in ("binned_delta", "binned_u16"):
             assert bool(stats["format"] & 32) == (expect_kernel == "binned_delta")
     return out, stats
@@ -1063,3 +1068,43 @@ def test_spmv_hw_adds_into_nonzero_y_fpga(torch, monkeypatch, units, prefault):
     lib.delete_csr_hw_matrix(hw)
     lib.free_bitmap(bm)
     lib.delete_csr_hw_x_vector(hx)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("shape", ["powerlaw", "sparse_cols"])
+def test_sweep_delta_columns(torch, monkeypatch, dtype, shape):
+    """Delta-coded sweep columns (format bit 6: a u16 row word + a u8 per entry holding the row and
+    a 9-bit column delta, a DPP prefix sum per wave instruction; chunks with a gap above 511 read
+    absolute columns from the side table). The same plan run on its 12-byte words (variant 35)
+    gives the same sums up to the LDS adds' order, and both match the oracle. "sparse_cols": 330K
+    rows (256 panels of ~1,290 rows) over 2M columns, ~97 columns between a panel's consecutive
+    entries, so about half the chunks hold a gap above 511 (side table) and half do not, and
+    gaps of 256-511 (bit 8 of the delta) are common. The power-law matrix of 10M columns sorts on
+    bucketed keys (shift 1), which the delta build re-sorts per chunk."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    monkeypatch.delenv("SPMV_SWEEP_DELTA", raising=False)
+    lib = spmv_hw.load(dtype)
+    if shape == "powerlaw":
+        n, m, z = 2_000_000, 10_000_000, 32_000_000
+    else:
+        n, m, z = 330_000, 2_000_000, 5_280_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, z, seed=8)
+    x = spmv_hw.gen_vector(lib, m, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, m)
+    st = plan.stats()
+    assert st["kernel"] == 2 and st["format"] & 64 and st["format"] & 2
+    ys = []
+    for variant in (28, 35):  # 28: the default on the 11-byte entries, 35: on the 12-byte words
+        plan.set_variant(variant)
+        y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+        plan.run(x, y)
+        torch.cuda.synchronize()
+        ys.append(y.cpu().numpy())
+    plan.destroy()
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref = oracle.spmv_fp64acc(row_ptr, c, v, xx) if dtype == np.float32 else oracle.spmv_gold(row_ptr, c, v, xx)
+    for y in ys:
+        assert not np.isnan(y).any()
+        assert oracle.scaled_error(row_ptr, c, v, xx, ref, y) <= TIGHT[np.dtype(dtype)]
+    assert oracle.scaled_error(row_ptr, c, v, xx, ys[1].astype(np.float64), ys[0]) <= TIGHT[np.dtype(dtype)]

@@ -52,8 +52,9 @@ def main():
     a = ap.parse_args()
     # measurement-only ablations live in the tools library only (spmv-fpga_amd Makefile target
     # `ablations`); the product library refuses them
-    abl = any((v.split(":")[0].startswith("sweep") and int(v.split(":")[1]) in range(51, 64))
+    abl = any((v.split(":")[0].startswith("sweep") and int(v.split(":")[1]) in range(50, 64))
               or (v.split(":")[0].startswith("blocked") and v.split(":")[1] == "1")
+              or (v.split(":")[0].startswith("binned") and int(v.split(":")[1]) in (51, 52))
               for v in a.variants.split(",") if ":" in v)
     if abl:
         os.environ["SPMV_HW_ABLATIONS"] = "1"
@@ -139,7 +140,7 @@ def main():
                 torch.cuda.synchronize()
                 if ref is None:
                     ref = y.clone()
-                elif int(var) not in (53, 54, 55, 60, 61, 62, 63) and not (k.startswith("blocked") and var == "1"):  # measurement-only ablations (wrong y)
+                elif int(var) not in (50, 51, 52, 53, 54, 55, 60, 61, 62, 63) and not (k.startswith("blocked") and var == "1"):  # measurement-only ablations (wrong y)
                     err = float(((ref - y).abs().max() / ref.abs().max().clamp_min(1e-300)).item())
                     assert err < (1e-9 if a.dtype == "f64" else 1e-5), f"{v} changed the result ({err})"
                 plan.set_timing(True)
