@@ -831,6 +831,35 @@ def main():
         res["x_broadcast_ms"] = round(spmv_dist.max_over_ranks((time.perf_counter() - tb0) * 1e3 / 3, dev), 4)
         assert torch.equal(xb, x)  # every rank generates the same x
         del xb
+        # a stream of SpMVs (right-hand sides, time steps): step k's gather runs on the
+        # collective's stream while step k + 1 computes (spmv_dist.pipelined_gather, double-
+        # buffered y). One SpMV's own gather cannot overlap its compute
+        maxc = int(counts.max())
+        bufs = [torch.zeros(maxc, dtype=y.dtype, device=dev) for _ in range(2)]
+        nloc = int(st["nr_rows"])
+
+        def step(k, yb):
+            plan.run(x, yb[:nloc], stream)
+
+        psteps = max(args.steps, 4)
+        spmv_dist.pipelined_gather(step, bufs, counts, 2)  # warm
+        torch.cuda.synchronize()
+        barrier(world)
+        tp0 = time.perf_counter()
+        yp = spmv_dist.pipelined_gather(step, bufs, counts, psteps)
+        torch.cuda.synchronize()
+        barrier(world)
+        res["pipelined_gather_ms_per_step"] = round(
+            spmv_dist.max_over_ranks((time.perf_counter() - tp0) * 1e3 / psteps, dev), 4)
+        res["pipelined_steps"] = psteps
+        res["e2e_gflops_pipelined_gather"] = round(2.0 * nnz_all / (res["pipelined_gather_ms_per_step"] * 1e-3) / 1e9, 2)
+        if rank == 0:  # the last step's gathered y against a plain gather of the same SpMV
+            y_chk = spmv_dist.exchange_gather(bufs[(psteps - 1) % 2][:nloc], counts)
+            res["pipelined_max_rel_diff"] = float(((yp.double() - y_chk.double()).abs().max()
+                                                   / y_chk.double().abs().max().clamp_min(1e-300)).item())
+        else:
+            spmv_dist.exchange_gather(bufs[(psteps - 1) % 2][:nloc], counts)
+        del bufs
         res["y_bytes"] = n_total * y.element_size()
         res["e2e_gflops_with_gather"] = round(2.0 * nnz_all / ((ms + res["gather_ms"]) * 1e-3) / 1e9, 2)
         res["e2e_gflops_with_reduce"] = round(2.0 * nnz_all / ((ms + res["reduce_ms"]) * 1e-3) / 1e9, 2)

@@ -82,6 +82,43 @@ def exchange_allgather(y_slice: torch.Tensor, counts, out: torch.Tensor | None =
     return out
 
 
+def pipelined_gather(run_step, y_bufs, counts, steps: int, dst: int = 0):
+    """`steps` independent SpMVs whose y exchange overlaps the next SpMV.
+
+    One SpMV's gather cannot overlap its own compute: the N = 8 slice is a single round of
+    workgroups whose rows all finish at the end. A stream of SpMVs (right-hand
+    sides, time steps) can: step k's y goes to rank `dst` on the collective's own stream while
+    step k + 1 computes into the other buffer of `y_bufs` (double buffering; a buffer is reused
+    only once its previous gather completed). run_step(k, y) enqueues SpMV k into y[:count] on the
+    current stream. y_bufs are two device tensors of max(counts) values (equal-size gather). On
+    rank `dst` returns the last step's full y; None elsewhere."""
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    maxc = int(max(counts))
+    assert len(y_bufs) == 2 and all(b.numel() == maxc for b in y_bufs)
+    gloo = dist.get_backend() == "gloo"
+    parts = [[torch.empty(maxc, dtype=y_bufs[0].dtype, device="cpu" if gloo else y_bufs[0].device)
+              for _ in range(world)] for _ in range(2)] if rank == dst else [None, None]
+    works = [None, None]
+    for k in range(steps):
+        b = k % 2
+        if works[b] is not None:
+            works[b].wait()  # this buffer's previous gather is done before it is overwritten
+        run_step(k, y_bufs[b])
+        src = _staged(y_bufs[b])
+        if rank == dst:
+            works[b] = dist.gather(src, gather_list=parts[b], dst=dst, async_op=True)
+        else:
+            works[b] = dist.gather(src, dst=dst, async_op=True)
+    for w in works:
+        if w is not None:
+            w.wait()
+    if rank != dst or steps == 0:
+        return None
+    last = parts[(steps - 1) % 2]
+    return torch.cat([last[r][:int(counts[r])] for r in range(world)])
+
+
 def broadcast_x(x: torch.Tensor, src: int = 0) -> torch.Tensor:
     """x replicated from rank `src` to every rank (broadcast once, then resident)."""
     buf = _staged(x)

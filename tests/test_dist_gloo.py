@@ -50,7 +50,18 @@ def _worker(rank, world, port, mode, q):
         rp = row_ptr[r0:r1 + 1]
         y_local = oracle.spmv_gold((rp - rp[0]).astype(np.uint32), col[rp[0]:rp[-1]], val[rp[0]:rp[-1]], x)
         y_t = torch.from_numpy(y_local)
-        if mode == "reduce":
+        if mode == "pipelined":
+            # 5 SpMVs, each of a different x (x scaled by k + 1), their gathers overlapping the
+            # next SpMV; the last step's y reaches rank 0 whole
+            counts = sdist.slice_counts(bounds)
+            sub = ((rp - rp[0]).astype(np.uint32), col[rp[0]:rp[-1]], val[rp[0]:rp[-1]])
+            bufs = [torch.zeros(int(max(counts)), dtype=torch.float64) for _ in range(2)]
+
+            def step(k, yb):
+                yb[:r1 - r0] = torch.from_numpy(oracle.spmv_gold(*sub, x * (k + 1)))
+
+            full = sdist.pipelined_gather(step, bufs, counts, 5)
+        elif mode == "reduce":
             full = sdist.exchange_reduce(y_t, r0, n)
         elif mode == "gather":
             full = sdist.exchange_gather(y_t, sdist.slice_counts(bounds))
@@ -62,7 +73,7 @@ def _worker(rank, world, port, mode, q):
         assert np.array_equal(xb.numpy(), x)
         m = sdist.max_over_ranks(float(rank), torch.device("cpu"))
         if rank == 0:
-            y_ref = oracle.spmv_gold(row_ptr, col, val, x)
+            y_ref = oracle.spmv_gold(row_ptr, col, val, x * 5 if mode == "pipelined" else x)  # last step: x * 5
             q.put((np.array_equal(full.numpy(), y_ref), m, list(sdist.slice_counts(bounds))))
         elif mode != "allgather":
             assert full is None
@@ -71,7 +82,7 @@ def _worker(rank, world, port, mode, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("mode", ["reduce", "gather", "allgather"])
+@pytest.mark.parametrize("mode", ["reduce", "gather", "allgather", "pipelined"])
 def test_row_sliced_exchange_rebuilds_y(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
