@@ -290,7 +290,8 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         const uint64_t val_bytes = stored * sizeof(ValueType);
         // the index stream of the unit's representation (opaque device address)
         h->sub[0] = pl.kernel == kKernelBinned ? reinterpret_cast<BusDataType *>(pl.d_b_colw)
-                    : sweep ? reinterpret_cast<BusDataType *>(pl.d_s_col)
+                    : sweep ? (pl.d_s_col ? reinterpret_cast<BusDataType *>(pl.d_s_col)
+                                          : reinterpret_cast<BusDataType *>(pl.d_s_row16))
                     : (slices || pl.kernel == kKernelBlocked || pl.tile_col_bytes < 4)
                         ? reinterpret_cast<BusDataType *>(pl.d_colnar)
                         : reinterpret_cast<BusDataType *>(pl.d_col);

@@ -680,7 +680,7 @@ uint64_t spmv_plan::device_bytes() const
         return ent_pad * (2 * sizeof(ValueType) + 2 + (b_delta ? 1 : 2)) + (uint64_t(b_nwin) * npanels + 1) * 8 +
                (b_nunits + 1) * 12 + (npanels + 1) * 4;
     if (kernel == kKernelSweep)
-        return ent_pad * (sizeof(uint32_t) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
+        return ent_pad * ((d_s_col ? sizeof(uint32_t) : 0) + (sweep_packed ? 0 : sizeof(uint16_t)) + sizeof(ValueType)) +
                (npanels + 1) * 4 + (nunits + 1) * 4 + (sweep_packed ? ent_pad / kSweepChunk * 4 : 0) +
                (sweep_split > 1 ? nunits * (uint64_t(panel_rmax) + 1) * sweep_acc_bytes : 0) + nunits * 4 + (npanels + 1) * 4 +
                (d_panel_cnt ? npanels * 4 : 0) +
@@ -900,6 +900,10 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
     }
 #endif
     if (p->kernel == kKernelSweep) {
+        // every variant but the default (28) reads the 12-byte rc words, which a delta plan
+        // rebuilds on first use
+        if (variant != 28 && sweep_materialize_rc(*p))
+            return 1;
         p->sweep_variant = variant;
     } else if (p->kernel == kKernelBinned) {
         // 1 / 2 (tests, same y): pass 2 reads segment offsets rebased so that they straddle 2^31 /

@@ -152,7 +152,8 @@ struct spmv_plan {
     bool sweep_det = false;          // env SPMV_SWEEP_DETERMINISTIC=1: ordered LDS adds (k_spmv_sweep_turn)
     // delta-coded columns (default for packed lane-ordered plans, env SPMV_SWEEP_DELTA=0 off): the
     // default kernel streams 11 B/entry fp64 (7 fp32) instead of 12 (8); the 12-byte rc words
-    // stay resident for the kernels that read them (deterministic variants, ablations)
+    // (d_s_col) are freed and rebuilt on demand for the kernels that read them
+    // (sweep_materialize_rc: deterministic variants, variant 35, ablations)
     uint16_t *d_s_row16 = nullptr;   // row in panel per entry (bits 0-14) + bit 8 of its delta (lane order)
     uint8_t *d_s_d8 = nullptr;       // low 8 bits of the column minus the previous entry's column of
                                      // the same wave instruction (the first from the chunk base)
@@ -263,6 +264,7 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s);
 int probe_locality(const IndexType *d_rp, const IndexType *d_col, IndexType n, hipStream_t s, double *frac);
+int sweep_materialize_rc(spmv_plan &p);  // delta plan: rebuild the 12-byte rc words (once)
 
 // plan.cpp helpers shared with the wrapper
 int upload_staged(void *dst, const void *src, size_t bytes, hipStream_t s);  // pageable H2D, synchronous

@@ -284,6 +284,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
 // wave instruction; a chunk's first entry counts from the chunk base dbase[c]. A 64-lane DPP
 // prefix sum turns the deltas into columns. A chunk with a gap above 511 (~1 in 10^5 on the
 // headline matrix) has bit 31 of dbase set and its absolute columns in `side` (uniform branch).
+// `rc` is not read (a delta plan frees its 12-byte words).
 template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double, bool DL = false>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
@@ -753,6 +754,46 @@ __global__ void k_sweep_delta_base(const uint32_t *__restrict__ rc, const uint32
     dbase[c] = 0x80000000u | k;
     for (uint64_t m = 0; m < kSweepChunk; ++m)
         side[(uint64_t)k * kSweepChunk + m] = cbase[c] + (rc[c * kSweepChunk + m] & 0xFFFFu);
+}
+
+// the 12-byte rc words of a delta plan, rebuilt from the delta arrays (one thread per chunk):
+// column offsets are the running sums of the 9-bit deltas in logical entry order, or side-table
+// columns minus the chunk base
+__global__ void k_sweep_delta_decode(const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
+                                     const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ cbase,
+                                     const uint32_t *__restrict__ side, uint64_t nchunks, uint32_t *__restrict__ rc)
+{
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks)
+        return;
+    constexpr int G = (int)kSweepChunk;
+    const uint32_t db = dbase[c];
+    uint32_t off = 0;
+    for (int k = 0; k < G; ++k) {
+        const uint64_t m = c * G + 2 * (k & 63) + (k >> 6);
+        const uint32_t rw = row16[m];
+        if (db & 0x80000000u)
+            off = side[(uint64_t)(db & 0x7FFFFFFFu) * G + (m - c * G)] - cbase[c];
+        else
+            off += (uint32_t)d8[m] | ((rw >> 15) << 8);
+        rc[m] = ((rw & 0x7FFFu) << 16) | off;
+    }
+}
+
+// A delta plan keeps only the 11-byte entries; a kernel that reads the 12-byte rc words (the
+// deterministic variants 91 / 94, variant 35, the ablations) gets them rebuilt here, once
+int sweep_materialize_rc(spmv_plan &p)
+{
+    if (!p.sweep_delta || p.d_s_col || p.ent_pad == 0)
+        return 0;
+    const uint64_t nchunks = p.ent_pad / kSweepChunk;
+    SPMV_TRY(hipSetDevice(p.device));
+    SPMV_TRY(hipMalloc((void **)&p.d_s_col, p.ent_pad * 4));
+    hipLaunchKernelGGL(k_sweep_delta_decode, dim3((unsigned)((nchunks + 63) / 64)), dim3(64), 0, nullptr, p.d_s_row16,
+                       p.d_s_d8, p.d_s_dbase, p.d_s_cbase, p.d_s_side, nchunks, p.d_s_col);
+    SPMV_TRY(hipGetLastError());
+    SPMV_TRY(hipDeviceSynchronize());
+    return 0;
 }
 
 // sort key of every entry: (panel, column bucket); one thread per row
@@ -1244,7 +1285,9 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                 p.d_s_val = v2;
                 p.sweep_lane_order = true;
                 // delta-coded columns for the default kernel (env SPMV_SWEEP_DELTA=0 keeps the
-                // 12-byte words only). The deterministic form reads the rc words, so it skips them
+                // 12-byte words only). SPMV_SWEEP_DETERMINISTIC=1 plans keep the 12-byte words:
+                // the turn kernel on the 11-byte entries measured 0.897 vs 0.871 ms (its deeper
+                // pipeline has no room for the decode, profiles/r03_delta_columns.jsonl r03p)
                 const char *de = std::getenv("SPMV_SWEEP_DELTA");
                 if (!(de && de[0] == '0') && !det && nchunks && uint64_t(p.nr_cols) < (1ull << 31) &&
                     rmax_used < 32768) {
@@ -1283,6 +1326,10 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                     (void)hipFree(d_sidx);
                     SW_TRY(e);
                     p.sweep_delta = true;
+                    // the default kernel reads only the 11-byte entries: the rc words are freed
+                    // (rebuilt by sweep_materialize_rc for a variant that reads them)
+                    SW_TRY(hipFree(p.d_s_col));
+                    p.d_s_col = nullptr;
                 }
             }
         } else {

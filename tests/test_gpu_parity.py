@@ -1108,3 +1108,44 @@ def test_sweep_delta_columns(torch, monkeypatch, dtype, shape):
         assert not np.isnan(y).any()
         assert oracle.scaled_error(row_ptr, c, v, xx, ref, y) <= TIGHT[np.dtype(dtype)]
     assert oracle.scaled_error(row_ptr, c, v, xx, ys[1].astype(np.float64), ys[0]) <= TIGHT[np.dtype(dtype)]
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sweep_delta_gap_edges(torch, monkeypatch, dtype):
+    """Column gaps at the edges of the delta encoding, in one panel whose column-sorted entries
+    form three chunks: chunk 0 cycles the gaps 0 (a repeated column), 1, 255, 256 and 511 (all
+    encodable: bit 8 of the delta rides in the row word); chunk 1 is the same plus one gap of 512
+    (the chunk reads the side table); chunk 2 has gaps of 256 and 511 only, ending in a partial
+    chunk (pad entries). y matches the oracle on the 11-byte and the 12-byte entries alike."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    monkeypatch.delenv("SPMV_SWEEP_DELTA", raising=False)
+    lib = spmv_hw.load(dtype)
+    cyc = [0, 1, 255, 256, 511]
+    gaps = [cyc[k % 5] for k in range(128)] + [cyc[k % 5] for k in range(127)] + [512] \
+        + [(256, 511)[k % 2] for k in range(100)]
+    cols = np.cumsum(np.array(gaps, np.int64)) + 7
+    z = len(cols)
+    n = 997
+    rows = (np.arange(z) * 7919) % n
+    order = np.lexsort((cols, rows))  # CSR: by row, then column
+    rows, cols = rows[order], cols[order]
+    row_ptr = np.zeros(n + 1, np.int64)
+    np.add.at(row_ptr, rows + 1, 1)
+    row_ptr = np.cumsum(row_ptr).astype(np.uint32)
+    m = int(cols.max()) + 1
+    rng = np.random.default_rng(3)
+    val = rng.uniform(-1, 1, z).astype(dtype)
+    x = rng.uniform(0, 1, m).astype(dtype)
+    col = cols.astype(np.uint32)
+    plan = spmv_hw.Plan.from_device(lib, to_dev(torch, row_ptr), to_dev(torch, col), to_dev(torch, val), m)
+    st = plan.stats()
+    assert st["kernel"] == 2 and st["format"] & 64, st
+    ref = oracle.spmv_gold(row_ptr, col, val, x)
+    xd = to_dev(torch, x)
+    for variant in (28, 35):
+        plan.set_variant(variant)
+        y = torch.full((n,), float("nan"), dtype=xd.dtype, device="cuda")
+        plan.run(xd, y)
+        torch.cuda.synchronize()
+        check(row_ptr, col, val, x, ref, y.cpu().numpy(), dtype)
+    plan.destroy()

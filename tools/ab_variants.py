@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--nnz", type=int, default=None)
+    ap.add_argument("--cols", type=int, default=None, help="power-law: columns (default = rows)")
     a = ap.parse_args()
     # measurement-only ablations live in the tools library only (spmv-fpga_amd Makefile target
     # `ablations`); the product library refuses them
@@ -62,6 +63,7 @@ def main():
     lib = spmv_hw.load(dtype)
     variants = [v if ":" in v else f"tiles:{v}" for v in a.variants.split(",")]
     for wl in a.workload.split(","):
+        mcols = None
         if wl == "banded":
             n = a.rows or 1_000_000
             rp, col, val = spmv_hw.gen_banded(lib, n, 16)
@@ -71,8 +73,10 @@ def main():
             x = spmv_hw.gen_vector(lib, n, seed=3)
         else:
             n = a.rows or 10_000_000
-            rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, a.nnz or 16 * n)
-            x = spmv_hw.gen_vector(lib, n, seed=6)
+            mcols = a.cols or n
+            rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, mcols, a.nnz or 16 * n)
+            x = spmv_hw.gen_vector(lib, mcols, seed=6)
+        mcols = mcols or n
         plans = {}
         for v in variants:
             k, var = v.split(":")
@@ -114,7 +118,7 @@ def main():
                 os.environ["SPMV_HW_KERNEL"] = kern
                 if threads:
                     os.environ["SPMV_SWEEP_THREADS"] = threads
-                plans[k] = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+                plans[k] = spmv_hw.Plan.from_device(lib, rp, col, val, mcols)
                 os.environ.pop("SPMV_SWEEP_THREADS", None)
                 os.environ.pop("SPMV_SWEEP_PACKED", None)
                 os.environ.pop("SPMV_SWEEP_LANE_ORDER", None)
