@@ -254,6 +254,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
     if (spmv_partition_rows(matrix->row_ptr, n, units, bounds.data()))
         die(spmv_hw_last_error());
 
+    const int merge = merge_mode(units);
     // null-terminated, and never shorter than the reference's largest CU count (+1)
     *hw_matrix = (csr_hw_matrix **)std::calloc(std::max(units, kMaxReferenceUnits) + 1, sizeof(csr_hw_matrix *));
     uint64_t in_bytes = 0, nnz_total = 0;
@@ -269,7 +270,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         // inside spmv_hw's timed region
         const hipStream_t us = unit_stream(u);
         const IndexType rows = h->row_end - h->row_begin;
-        if (rows) {
+        if (rows && merge == kMergeHost) {  // the RCCL merge stages the whole y instead (below)
             alloc_y_scratch(h);
             // full size: large copies take a different path whose first use costs ~20 ms
             check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
@@ -315,10 +316,10 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         std::lock_guard<std::mutex> lk(g_mu);
         g_units_max = std::max(g_units_max, units);
     }
-    if (const int mode = merge_mode(units); mode != kMergeHost) {
+    if (merge != kMergeHost) {
         // the clique is formed here (ncclCommInitAll), outside spmv_hw's timed region
         auto *c = new hw_clique();
-        c->mode = mode;
+        c->mode = merge;
         std::vector<const spmv_plan *> plans(units);
         for (int u = 0; u < units; ++u) {
             c->devices.push_back(impl((*hw_matrix)[u])->device);
@@ -330,6 +331,12 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         check(hipSetDevice(c->devices[0]), "hipSetDevice");
         check(hipHostMalloc((void **)&c->h_full, std::max<uint64_t>(n, 1) * sizeof(ValueType), hipHostMallocDefault),
               "hipHostMalloc(y stage)");
+        if (n) {  // first large D2H copy here, not in the first spmv_hw (as for the host merge)
+            check(hipMemcpyAsync(c->h_full, mgpu_root_y(c->mg), size_t(n) * sizeof(ValueType), hipMemcpyDeviceToHost,
+                                 unit_stream(0)),
+                  "warm D2H");
+            check(hipStreamSynchronize(unit_stream(0)), "warm D2H");
+        }
         impl((*hw_matrix)[0])->clique = c;
     }
     // empty_rows_bitmap[block][row] (csr_hw.cpp:391-393, :340-347): inner rows live inside the
@@ -422,7 +429,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
             die("spmv_hw: y_fpga is shorter than the matrix has rows");
         if ((size_t)m->device >= x->per_device.size())
             die("spmv_hw: x vector was not uploaded to device " + std::to_string(m->device));
-        if (rows && !m->d_y)
+        if (rows && !m->d_y && !impl(hw_matrix[0])->clique)
             alloc_y_scratch(m);
     }
 
