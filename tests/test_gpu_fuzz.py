@@ -17,9 +17,10 @@ from test_gpu_parity import KERNEL_ID, _bitwise, check, run_device
 pytestmark = pytest.mark.gpu
 
 SEEDS = list(range(48))
-FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_unpacked", "sweep_det", "gold", "slices", "slices_wide",
+FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_rc", "sweep_unpacked", "sweep_det", "gold", "slices", "slices_wide",
                 "slices_acc32", "fpga", "blocked", "binned", "binned_delta", "auto", "tune"]
 ENV = {"tiles_wide": {"SPMV_TILE_NARROW": "0"}, "sweep_unpacked": {"SPMV_SWEEP_PACKED": "0"},
+       "sweep_rc": {"SPMV_SWEEP_DELTA": "0"},
        "sweep_det": {"SPMV_SWEEP_DETERMINISTIC": "1"},
        "slices_wide": {"SPMV_SLICE_NARROW": "0"}, "slices_acc32": {"SPMV_SLICE_ACC": "32"},
        "binned_delta": {"SPMV_BIN_DELTA": "1"}}
