@@ -145,7 +145,10 @@ int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
  * (3 % faster; relies on the LDS executing a CU's requests in arrival order). Unpacked entries (a chunk spans >= 65536 columns):
  * 0/1/3/7/15/22 and the default (4 groups of 2 per barrier). Slices (kernel 5): 0 = 4 slot
  * pairs per iteration (default), 1 = 2, 2 = 7, 3 = 4 re-reading past the slice's end.
- * Blocked (kernel 4): 1 = measurement-only ablation, partials stored in compact order (wrong y). */
+ * Blocked (kernel 4): 1 = measurement-only ablation, partials stored in compact order (wrong y).
+ * Binned (kernel 6): 1 / 2 = segment offsets rebased past 2^31 / 2^32 (tests; same y), 3 / 4 / 5 =
+ * pass 1 with temporal product stores / entry loads / both, 6 = non-temporal product stores
+ * (same y; 0 = the plan's choice: temporal stores when the products take <= 1 GiB). */
 int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */

@@ -80,7 +80,9 @@ template <> struct BinDelta<2> { typedef uint16_t T; };
 
 // Pass 1: unit u = entries [ub[u], ub[u+1]) of window uwin[u] (both multiples of PER).
 // AL: x is 16-byte aligned, so the window is staged with 16-byte loads.
-template <typename V, bool AL>
+// POL (variants 3-5, the same y): bit 0 = temporal (default-policy) product stores instead of
+// non-temporal ones, bit 1 = temporal entry loads
+template <typename V, bool AL, int POL = 0>
 __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint32_t ncols, uint32_t W,
                                                    const uint64_t *__restrict__ ub, const uint32_t *__restrict__ uwin,
                                                    const uint16_t *__restrict__ colw, const V *__restrict__ val,
@@ -141,8 +143,13 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
         for (int k = 0; k < kBinU; ++k) {
             const uint64_t i = s + k * STEP + lane * PER;
             if (i < e1) {
-                v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + i));
-                c[k] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(colw + i));
+                if constexpr (POL & 2) {
+                    v[k] = *reinterpret_cast<const VT *>(val + i);
+                    c[k] = *reinterpret_cast<const IT *>(colw + i);
+                } else {
+                    v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(val + i));
+                    c[k] = __builtin_nontemporal_load(reinterpret_cast<const IT *>(colw + i));
+                }
             }
         }
 #pragma unroll
@@ -156,7 +163,10 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
                     const V xq = xs[cq == kBinSent ? 0 : cq];
                     pr[q] = cq == kBinSent ? V(0) : v[k][q] * xq;
                 }
-                __builtin_nontemporal_store(pr, reinterpret_cast<VT *>(prod + i));
+                if constexpr (POL & 1)
+                    *reinterpret_cast<VT *>(prod + i) = pr;
+                else
+                    __builtin_nontemporal_store(pr, reinterpret_cast<VT *>(prod + i));
             }
         }
     }
@@ -447,7 +457,20 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
     if (p.b_nunits) {
         const size_t lds1 = size_t(p.b_W) * sizeof(ValueType);
         const bool al = (reinterpret_cast<uintptr_t>(d_x) & 15u) == 0;
-        if (al || warm)
+        // pass-1 cache policy: temporal product stores when the products fit well within
+        // reach of the 256 MB MALL (fp32 10M/160M: 640 MB, 0.460 vs 0.487 ms; fp64 1.28 GB:
+        // 0.852 vs 0.835, profiles/r03s_binned_policy.jsonl); variants 3-5 force a policy, 6 the
+        // non-temporal stores
+        const int pol = p.variant >= 3 && p.variant <= 5 ? p.variant - 2
+                        : p.variant == 6                ? 0
+                                                        : (p.b_prod_temporal ? 1 : 0);
+        if (pol && al) {
+#define BINPOL(P)                                                                                          \
+    launch_or_warm(warm, k_bin_mul<ValueType, true, P>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x, \
+                   (uint32_t)p.nr_cols, p.b_W, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod)
+            if (pol == 1) BINPOL(1); else if (pol == 2) BINPOL(2); else BINPOL(3);
+#undef BINPOL
+        } else if (al || warm)
             launch_or_warm(warm, k_bin_mul<ValueType, true>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x,
                            (uint32_t)p.nr_cols, p.b_W, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
         if (!al || warm)
@@ -693,6 +716,7 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     }
     const uint64_t ent_pad = seg[nseg];
     p.ent_pad = ent_pad;
+    p.b_prod_temporal = ent_pad * sizeof(ValueType) <= (1ull << 30);
     std::vector<uint64_t> ub(1, 0);
     std::vector<uint32_t> uwin;
     {

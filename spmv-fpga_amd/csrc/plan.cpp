@@ -909,9 +909,11 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
         // 1 / 2 (tests, same y): pass 2 reads segment offsets rebased so that they straddle 2^31 /
         // 2^32 entries (prod and rowp rebased the other way: the same addresses), which drives the
         // 64-bit bound widening after readlane (binned.hip, k_bin_acc) without a 2^31-entry matrix
-        // 51 / 52 (tools library): pass-2 ablations, binned.hip
-        if (variant > 2 && !(variant >= 51 && variant <= 52)) {
-            set_error("spmv_plan_set_variant: binned variants are 0, 1 and 2");
+        // 3-6 (same y): pass-1 cache policy (3: temporal product stores, 4: temporal entry
+        // loads, 5: both, 6: non-temporal stores; 0 = the plan's choice); 51 / 52 (tools
+        // library): pass-2 ablations, binned.hip
+        if (variant > 6 && !(variant >= 51 && variant <= 52)) {
+            set_error("spmv_plan_set_variant: binned variants are 0-6");
             return 1;
         }
         if (p->d_b_seg_hi) {

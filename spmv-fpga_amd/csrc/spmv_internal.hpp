@@ -169,6 +169,8 @@ struct spmv_plan {
     uint16_t *d_b_colw = nullptr;      // column - window base
     void *d_b_rowp = nullptr;          // u16 row - panel base, or (b_delta) u8 row deltas
     bool b_delta = false;              // segments sorted by row, 1-byte deltas (binned.hip)
+    bool b_prod_temporal = false;      // pass 1 stores the products with the default cache policy
+                                       // (they stay partly in MALL for pass 2): products <= 1 GiB
     ValueType *d_b_prod = nullptr;     // products, written by pass 1 and read by pass 2
     uint64_t *d_b_seg = nullptr;       // padded segment offsets [b_nwin * npanels + 1]
     uint64_t *d_b_seg_hi = nullptr;    // variants 1 / 2 (tests): d_b_seg + b_seg_base, read by pass 2
