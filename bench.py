@@ -471,6 +471,10 @@ def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
             es.append(e)
         res[f"{name}_compute_ms"] = round(spmv_dist.max_over_ranks(float(np.median(cs)), dev), 5)
         res[f"{name}_exchange_ms"] = round(spmv_dist.max_over_ranks(float(np.median(es)), dev), 5)
+        if mode != spmv_hw.MGPU_ALLGATHER:  # a stream of SpMVs, each exchange under the next kernels
+            mg.run_pipelined(mode, 2)
+            res[f"{name}_pipelined_ms_per_step"] = round(
+                spmv_dist.max_over_ranks(mg.run_pipelined(mode, max(reps, 8)), dev), 5)
         if mode == spmv_hw.MGPU_GATHER:
             y_loc = torch.empty(int(counts[rank]), dtype=x.dtype, device=dev)
             plan.run(x, y_loc, torch.cuda.current_stream())

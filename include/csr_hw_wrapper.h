@@ -178,6 +178,11 @@ int spmv_mgpu_create(spmv_mgpu **mg, int ndev, const int *devices, const csr_mat
 int spmv_mgpu_set_x(spmv_mgpu *mg, const ValueType *h_x);
 /* the SpMV on every device, then the `exchange` (SPMV_MGPU_*) */
 int spmv_mgpu_run(spmv_mgpu *mg, int exchange);
+/* `steps` SpMVs of the handle's x, the exchange (SPMV_MGPU_GATHER or _REDUCE) of step k on a
+ * second stream overlapping the kernels of step k + 1 (double-buffered y); rank 0's y then holds
+ * the last step's result. *ms_per_step = first kernel to last exchange / steps (this process's
+ * devices, max). For a stream of SpMVs; one SpMV's exchange cannot overlap its own kernels. */
+int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_per_step);
 /* y[nr_rows] of the last run to host memory (pass the exchange form of that run) */
 int spmv_mgpu_get_y(spmv_mgpu *mg, ValueType *h_y, int exchange);
 /* last run: kernels (max over devices) and exchange time, ms (HIP events on each device) */

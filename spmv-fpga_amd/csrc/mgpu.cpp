@@ -113,6 +113,15 @@ struct spmv_mgpu {
     std::vector<ValueType *> y;         // rank 0 only: the full y
     std::vector<hipEvent_t> ev;         // per device: start, kernels done, exchange done
     double compute_ms = 0, exchange_ms = 0;
+    // spmv_mgpu_run_pipelined: per device a second stream for the exchange, a second y buffer
+    // (and reduce partial), and the events that hand each buffer between the two streams
+    struct Pipe {
+        hipStream_t cs = nullptr;
+        ValueType *buf2 = nullptr;   // second y: the root's full y / a rank's slice / reduce output
+        ValueType *part2 = nullptr;  // reduce: second full-length partial
+        hipEvent_t comp[2] = {nullptr, nullptr}, exch[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr;
+    };
+    std::vector<Pipe> pipe;
 
     void init(int n)
     {
@@ -145,6 +154,17 @@ struct spmv_mgpu {
             for (int k = 0; k < 3; ++k)
                 if (ev[3 * d + k])
                     (void)hipEventDestroy(ev[3 * d + k]);
+            if (d < (int)pipe.size()) {
+                Pipe &q = pipe[d];
+                for (void *p : {(void *)q.buf2, (void *)q.part2})
+                    if (p)
+                        (void)hipFree(p);
+                for (hipEvent_t e : {q.comp[0], q.comp[1], q.exch[0], q.exch[1], q.t0, q.t1})
+                    if (e)
+                        (void)hipEventDestroy(e);
+                if (q.cs)
+                    (void)hipStreamDestroy(q.cs);
+            }
         }
     }
     IndexType rows_of(int r) const { return bounds[r + 1] - bounds[r]; }
@@ -553,6 +573,126 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange)
         return 1;
     }
     return mgpu_run_on(mg, exchange, nullptr);
+}
+
+// `steps` SpMVs of the handle's x with the exchange of step k overlapping the kernels of step
+// k + 1: the kernels run on each device's stream into one of two y buffers,
+// the exchange (gather or reduce) on a second stream after an event, and a buffer is reused only
+// once its exchange completed. One SpMV's own exchange cannot overlap its kernels: a slice of the
+// strong-scaling matrix runs as one round of workgroups whose rows all finish at the end
+// (DESIGN.md §6). Afterwards rank 0's y holds the last step's result (spmv_mgpu_get_y /
+// spmv_mgpu_y_device with the same exchange). *ms_per_step: first kernel to last exchange, max
+// over this process's devices, / steps.
+int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_per_step)
+{
+    if (!mg || !mg->own_x || steps < 1 || (exchange != SPMV_MGPU_GATHER && exchange != SPMV_MGPU_REDUCE)) {
+        set_error("spmv_mgpu_run_pipelined: bad arguments (gather or reduce, steps >= 1)");
+        return 1;
+    }
+    const int nl = mg->nloc, nr = mg->nranks;
+    const bool red = exchange == SPMV_MGPU_REDUCE;
+    const size_t nb = size_t(mg->nr_rows) * sizeof(ValueType);
+    if (mg->pipe.empty())
+        mg->pipe.resize(nl);
+    for (int d = 0; d < nl; ++d) {  // resources on first use
+        SPMV_TRY(hipSetDevice(mg->dev[d]));
+        spmv_mgpu::Pipe &q = mg->pipe[d];
+        if (!q.cs) {
+            SPMV_TRY(hipStreamCreateWithFlags(&q.cs, hipStreamNonBlocking));
+            for (int b = 0; b < 2; ++b) {
+                SPMV_TRY(hipEventCreateWithFlags(&q.comp[b], hipEventDisableTiming));
+                SPMV_TRY(hipEventCreateWithFlags(&q.exch[b], hipEventDisableTiming));
+            }
+            SPMV_TRY(hipEventCreate(&q.t0));
+            SPMV_TRY(hipEventCreate(&q.t1));
+        }
+        const size_t yb = mg->rank[d] == 0 ? nb : size_t(mg->rows(d)) * sizeof(ValueType);
+        if (!q.buf2)
+            SPMV_TRY(hipMalloc((void **)&q.buf2, std::max<size_t>(std::max(yb, nb), sizeof(ValueType))));
+        if (red && !mg->ypart[d])
+            SPMV_TRY(hipMalloc((void **)&mg->ypart[d], std::max<size_t>(nb, sizeof(ValueType))));
+        if (red && !q.part2)
+            SPMV_TRY(hipMalloc((void **)&q.part2, std::max<size_t>(nb, sizeof(ValueType))));
+    }
+    // buffer b of device d: where its kernels write, and what the exchange sends / receives into
+    auto out = [&](int d, int b) -> ValueType * {  // rank 0's full y (gather and reduce output)
+        return b == 0 ? mg->y[d] : mg->pipe[d].buf2;
+    };
+    auto slice = [&](int d, int b) -> ValueType * {  // gather, rank > 0: its rows
+        return b == 0 ? mg->yslice[d] : mg->pipe[d].buf2;
+    };
+    auto part = [&](int d, int b) -> ValueType * {  // reduce: full-length partial
+        return b == 0 ? mg->ypart[d] : mg->pipe[d].part2;
+    };
+    for (int d = 0; d < nl; ++d) {
+        SPMV_TRY(hipSetDevice(mg->dev[d]));
+        SPMV_TRY(hipEventRecord(mg->pipe[d].t0, mg->stream[d]));
+    }
+    for (int k = 0; k < steps; ++k) {
+        const int b = k & 1;
+        for (int d = 0; d < nl; ++d) {
+            SPMV_TRY(hipSetDevice(mg->dev[d]));
+            spmv_mgpu::Pipe &q = mg->pipe[d];
+            hipStream_t s = mg->stream[d];
+            if (k >= 2)  // buffer b is free once the exchange of step k - 2 completed
+                SPMV_TRY(hipStreamWaitEvent(s, q.exch[b], 0));
+            ValueType *dst;
+            if (red) {
+                SPMV_TRY(hipMemsetAsync(part(d, b), 0, nb, s));
+                dst = part(d, b) + mg->bounds[mg->rank[d]];
+            } else {
+                dst = mg->rank[d] == 0 ? out(d, b) + mg->bounds[0] : slice(d, b);
+            }
+            if (mg->rows(d) && spmv_plan_run(mg->plan[d], mg->x[d], dst, s))
+                return 1;
+            SPMV_TRY(hipEventRecord(q.comp[b], s));
+            SPMV_TRY(hipStreamWaitEvent(q.cs, q.comp[b], 0));
+        }
+        if ((nr > 1 || red) && mg->nr_rows) {
+            MG_NCCL(mg->nc->GroupStart());
+            for (int d = 0; d < nl; ++d) {
+                hipStream_t cs = mg->pipe[d].cs;
+                const int rk = mg->rank[d];
+                if (red) {
+                    MG_NCCL(mg->nc->Reduce(part(d, b), rk == 0 ? out(d, b) : nullptr, mg->nr_rows, kNcclValue, ncclSum,
+                                           0, mg->comm[d], cs));
+                } else if (rk == 0) {
+                    for (int p = 1; p < nr; ++p)
+                        if (mg->rows_of(p))
+                            MG_NCCL(mg->nc->Recv(out(d, b) + mg->bounds[p], mg->rows_of(p), kNcclValue, p, mg->comm[d], cs));
+                } else if (mg->rows(d)) {
+                    MG_NCCL(mg->nc->Send(slice(d, b), mg->rows(d), kNcclValue, 0, mg->comm[d], cs));
+                }
+            }
+            MG_NCCL(mg->nc->GroupEnd());
+        }
+        for (int d = 0; d < nl; ++d) {
+            SPMV_TRY(hipSetDevice(mg->dev[d]));
+            SPMV_TRY(hipEventRecord(mg->pipe[d].exch[b], mg->pipe[d].cs));
+        }
+    }
+    double tmax = 0;
+    for (int d = 0; d < nl; ++d) {
+        SPMV_TRY(hipSetDevice(mg->dev[d]));
+        spmv_mgpu::Pipe &q = mg->pipe[d];
+        SPMV_TRY(hipStreamWaitEvent(q.cs, mg->pipe[d].comp[(steps - 1) & 1], 0));
+        SPMV_TRY(hipEventRecord(q.t1, q.cs));
+    }
+    for (int d = 0; d < nl; ++d) {
+        SPMV_TRY(hipSetDevice(mg->dev[d]));
+        SPMV_TRY(hipEventSynchronize(mg->pipe[d].t1));
+        float t = 0;
+        SPMV_TRY(hipEventElapsedTime(&t, mg->pipe[d].t0, mg->pipe[d].t1));
+        tmax = std::max(tmax, (double)t);
+        SPMV_TRY(hipStreamSynchronize(mg->stream[d]));
+    }
+    if ((steps - 1) & 1)  // the last result sits in the second buffers: make them rank 0's y
+        for (int d = 0; d < nl; ++d)
+            if (mg->rank[d] == 0)
+                std::swap(mg->y[d], mg->pipe[d].buf2);
+    if (ms_per_step)
+        *ms_per_step = tmax / steps;
+    return 0;
 }
 
 // y (nr_rows values) to the host: rank 0's y after a gather / reduce, any rank's x after an

@@ -104,7 +104,7 @@ EXPORTS = [
     "spmv_read_csr_header", "spmv_read_csr_matrix", "spmv_read_csr", "spmv_free_csr",
     "spmv_mgpu_create", "spmv_mgpu_set_x", "spmv_mgpu_run", "spmv_mgpu_get_y", "spmv_mgpu_get_timing",
     "spmv_mgpu_slice", "spmv_mgpu_destroy", "spmv_mgpu_unique_id", "spmv_mgpu_create_rank",
-    "spmv_mgpu_set_x_device", "spmv_mgpu_set_x_device_on", "spmv_mgpu_y_device",
+    "spmv_mgpu_set_x_device", "spmv_mgpu_set_x_device_on", "spmv_mgpu_y_device", "spmv_mgpu_run_pipelined",
 ]
 
 MGPU_GATHER, MGPU_REDUCE, MGPU_ALLGATHER = 0, 1, 2  # include/csr_hw_wrapper.h SPMV_MGPU_*
@@ -178,6 +178,7 @@ class Lib:
                                                      ctypes.c_int, up, IndexType, vp]),
             "spmv_mgpu_set_x_device": (ctypes.c_int, [vp, vp]),
             "spmv_mgpu_set_x_device_on": (ctypes.c_int, [vp, vp, vp]),
+            "spmv_mgpu_run_pipelined": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
             "spmv_mgpu_y_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp)]),
         }
         for name, (res, args) in sig.items():
@@ -416,6 +417,13 @@ class MultiGpu:
         sp = ctypes.c_void_p(stream.cuda_stream if stream is not None else 0)
         self.lib._ok(self.lib.L.spmv_mgpu_set_x_device_on(self.h, ctypes.c_void_p(x.data_ptr() if x is not None else 0),
                                                           sp), "spmv_mgpu_set_x_device_on")
+
+    def run_pipelined(self, exchange: int = MGPU_GATHER, steps: int = 8) -> float:
+        """`steps` SpMVs, each exchange overlapping the next SpMV's kernels; ms per step."""
+        ms = ctypes.c_double()
+        self.lib._ok(self.lib.L.spmv_mgpu_run_pipelined(self.h, int(exchange), int(steps), ctypes.byref(ms)),
+                     "spmv_mgpu_run_pipelined")
+        return float(ms.value)
 
     def y_device_ptr(self, exchange: int = MGPU_GATHER) -> int:
         p = ctypes.c_void_p()

@@ -172,3 +172,25 @@ def test_mgpu_set_x_device_waits_for_the_producer(form):
     assert oracle.scaled_error(r, c, h[2], h[3], ref, y) <= 1e-12
     mg.destroy()
     plan.destroy()
+
+
+@pytest.mark.parametrize("exchange", [spmv_hw.MGPU_GATHER, spmv_hw.MGPU_REDUCE])
+@pytest.mark.parametrize("steps", [1, 4, 5])
+def test_mgpu_run_pipelined(exchange, steps):
+    """spmv_mgpu_run_pipelined: `steps` SpMVs whose exchanges overlap the next SpMV's kernels
+    (double-buffered y; an even step count leaves the result in the second buffer, which then
+    becomes rank 0's y). The result equals the oracle and a plain run afterwards still works."""
+    lib = spmv_hw.load(np.float64)
+    n, z = 300_000, 4_800_000
+    rp, col, val, x = _powerlaw_host(lib, n, z)
+    mg = spmv_hw.MultiGpu(lib, lib.make_csr_matrix(rp, col, val, n), ndev=_ndev())
+    mg.set_x(x)
+    ref = oracle.spmv_gold(rp, col, val, x)
+    ms = mg.run_pipelined(exchange, steps)
+    assert ms > 0
+    assert oracle.scaled_error(rp, col, val, x, ref, mg.y(exchange)) <= 1e-12
+    mg.run(exchange)
+    assert oracle.scaled_error(rp, col, val, x, ref, mg.y(exchange)) <= 1e-12
+    with pytest.raises(RuntimeError, match="gather or reduce"):
+        mg.run_pipelined(spmv_hw.MGPU_ALLGATHER, 2)
+    mg.destroy()
