@@ -484,6 +484,13 @@ def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
                 y_n = torch.from_numpy(mg.y(spmv_hw.MGPU_GATHER)).to(y_t.device)
                 res["gather_max_rel_diff_vs_torch"] = float(
                     ((y_n.double() - y_t.double()).abs().max() / y_t.double().abs().max().clamp_min(1e-300)).item())
+    # iterative use: SpMV + all-gather of y into every rank's next x, steps
+    # replayed from one hipGraph per rank (spmv_mgpu_run_graph; capture outside the timing)
+    mg.set_x_device(x)
+    mg.run_graph(spmv_hw.MGPU_ALLGATHER, max(reps, 8))
+    mg.set_x_device(x)
+    res["allgather_graph_ms_per_step"] = round(
+        spmv_dist.max_over_ranks(mg.run_graph(spmv_hw.MGPU_ALLGATHER, max(reps, 8)), dev), 5)
     mg.destroy()
     return res
 

@@ -183,6 +183,12 @@ int spmv_mgpu_run(spmv_mgpu *mg, int exchange);
  * the last step's result. *ms_per_step = first kernel to last exchange / steps (this process's
  * devices, max). For a stream of SpMVs; one SpMV's exchange cannot overlap its own kernels. */
 int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_per_step);
+/* `iters` steps (SpMV + exchange) replayed from one hipGraph (captured on first use; re-captured
+ * when exchange, iters or the x buffer change), for a handle driving ONE device (one process per
+ * GPU, or a one-device clique). SPMV_MGPU_ALLGATHER iterates x <- A x and leaves A^iters x as the
+ * handle's x (spmv_mgpu_get_y / _y_device with ALLGATHER); gather / reduce repeat y = A x.
+ * *ms_per_step = the graph's duration / iters. */
+int spmv_mgpu_run_graph(spmv_mgpu *mg, int exchange, int iters, double *ms_per_step);
 /* y[nr_rows] of the last run to host memory (pass the exchange form of that run) */
 int spmv_mgpu_get_y(spmv_mgpu *mg, ValueType *h_y, int exchange);
 /* last run: kernels (max over devices) and exchange time, ms (HIP events on each device) */

@@ -122,6 +122,11 @@ struct spmv_mgpu {
         hipEvent_t comp[2] = {nullptr, nullptr}, exch[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr;
     };
     std::vector<Pipe> pipe;
+    // spmv_mgpu_run_graph (one device per handle): `g_iters` steps of kernels + exchange captured
+    // into one hipGraph, re-captured when the exchange, the step count or the x buffer changes
+    hipGraphExec_t gexec = nullptr;
+    int g_exchange = -1, g_iters = 0;
+    const ValueType *g_x = nullptr;
 
     void init(int n)
     {
@@ -154,6 +159,8 @@ struct spmv_mgpu {
             for (int k = 0; k < 3; ++k)
                 if (ev[3 * d + k])
                     (void)hipEventDestroy(ev[3 * d + k]);
+            if (d == 0 && gexec)
+                (void)hipGraphExecDestroy(gexec);
             if (d < (int)pipe.size()) {
                 Pipe &q = pipe[d];
                 for (void *p : {(void *)q.buf2, (void *)q.part2})
@@ -692,6 +699,108 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
                 std::swap(mg->y[d], mg->pipe[d].buf2);
     if (ms_per_step)
         *ms_per_step = tmax / steps;
+    return 0;
+}
+
+// one step of a one-device handle on stream s: the kernels on x_in, then the exchange; the
+// all-gather writes every slice of the next x into x_out (capturable: kernels, a memset and
+// RCCL calls only)
+static int enqueue_step(spmv_mgpu *mg, int exchange, const ValueType *x_in, ValueType *x_out, hipStream_t s)
+{
+    const int rk = mg->rank[0], nr = mg->nranks;
+    const size_t nb = size_t(mg->nr_rows) * sizeof(ValueType);
+    const IndexType b0 = mg->bounds[rk];
+    ValueType *dst = exchange == 2 ? x_out + b0 : exchange == 1 ? mg->ypart[0] + b0 : rk == 0 ? mg->y[0] + b0 : mg->yslice[0];
+    if (exchange == 1)
+        SPMV_TRY(hipMemsetAsync(mg->ypart[0], 0, nb, s));
+    if (mg->rows(0) && spmv_plan_run(mg->plan[0], x_in, dst, s))
+        return 1;
+    if ((nr > 1 || exchange == 1) && mg->nr_rows) {
+        MG_NCCL(mg->nc->GroupStart());
+        if (exchange == 0) {
+            if (rk == 0) {
+                for (int p = 1; p < nr; ++p)
+                    if (mg->rows_of(p))
+                        MG_NCCL(mg->nc->Recv(mg->y[0] + mg->bounds[p], mg->rows_of(p), kNcclValue, p, mg->comm[0], s));
+            } else if (mg->rows(0)) {
+                MG_NCCL(mg->nc->Send(mg->yslice[0], mg->rows(0), kNcclValue, 0, mg->comm[0], s));
+            }
+        } else if (exchange == 1) {
+            MG_NCCL(mg->nc->Reduce(mg->ypart[0], rk == 0 ? mg->y[0] : nullptr, mg->nr_rows, kNcclValue, ncclSum, 0,
+                                   mg->comm[0], s));
+        } else {
+            for (int r = 0; r < nr; ++r)
+                if (mg->rows_of(r))
+                    MG_NCCL(mg->nc->Broadcast(x_out + mg->bounds[r], x_out + mg->bounds[r], mg->rows_of(r), kNcclValue, r,
+                                              mg->comm[0], s));
+        }
+        MG_NCCL(mg->nc->GroupEnd());
+    }
+    return 0;
+}
+
+// `iters` steps (SpMV + exchange) replayed from one hipGraph, for a handle that drives one
+// device (one process per GPU, or a one-device clique): no host launch between the kernels and
+// the RCCL exchange or between steps. The all-gather form iterates x <- A x (the iterative use
+// of SURVEY §8f rank 3) and leaves A^iters x as this handle's x; gather / reduce repeat y = A x.
+// *ms_per_step: the graph's duration / iters (HIP events on the handle's stream).
+int spmv_mgpu_run_graph(spmv_mgpu *mg, int exchange, int iters, double *ms_per_step)
+{
+    if (!mg || !mg->own_x || iters < 1 || exchange < 0 || exchange > 2) {
+        set_error("spmv_mgpu_run_graph: bad arguments");
+        return 1;
+    }
+    if (mg->nloc != 1) {
+        set_error("spmv_mgpu_run_graph: graph capture needs a handle that drives one device");
+        return 1;
+    }
+    if (exchange == 2 && mg->nr_rows != mg->nr_cols) {
+        set_error("spmv_mgpu_run_graph: the all-gather exchange makes y the next x (needs a square matrix)");
+        return 1;
+    }
+    const size_t nb = std::max<size_t>(size_t(mg->nr_rows) * sizeof(ValueType), sizeof(ValueType));
+    SPMV_TRY(hipSetDevice(mg->dev[0]));
+    if (exchange == 1 && !mg->ypart[0])
+        SPMV_TRY(hipMalloc((void **)&mg->ypart[0], nb));
+    if (exchange == 2 && !mg->xnext[0])
+        SPMV_TRY(hipMalloc((void **)&mg->xnext[0], nb));
+    hipStream_t s = mg->stream[0];
+    if (!mg->gexec || mg->g_exchange != exchange || mg->g_iters != iters || mg->g_x != mg->x[0]) {
+        if (mg->gexec) {
+            SPMV_TRY(hipGraphExecDestroy(mg->gexec));
+            mg->gexec = nullptr;
+        }
+        SPMV_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        int rc = 0;
+        for (int i = 0; i < iters && !rc; ++i) {
+            const bool odd = exchange == 2 && (i & 1);
+            rc = enqueue_step(mg, exchange, odd ? mg->xnext[0] : mg->x[0], odd ? mg->x[0] : mg->xnext[0], s);
+        }
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(s, &g);
+        if (rc) {
+            if (g)
+                (void)hipGraphDestroy(g);
+            return rc;
+        }
+        SPMV_TRY(ec);
+        const hipError_t ei = hipGraphInstantiate(&mg->gexec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        SPMV_TRY(ei);
+        mg->g_exchange = exchange;
+        mg->g_iters = iters;
+        mg->g_x = mg->x[0];
+    }
+    SPMV_TRY(hipEventRecord(mg->ev[0], s));
+    SPMV_TRY(hipGraphLaunch(mg->gexec, s));
+    SPMV_TRY(hipEventRecord(mg->ev[2], s));
+    SPMV_TRY(hipEventSynchronize(mg->ev[2]));
+    float t = 0;
+    SPMV_TRY(hipEventElapsedTime(&t, mg->ev[0], mg->ev[2]));
+    if (ms_per_step)
+        *ms_per_step = double(t) / iters;
+    if (exchange == 2 && (iters & 1))  // the last y sits in the other buffer: make it x
+        std::swap(mg->x[0], mg->xnext[0]);
     return 0;
 }
 

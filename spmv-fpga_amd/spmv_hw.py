@@ -105,6 +105,7 @@ EXPORTS = [
     "spmv_mgpu_create", "spmv_mgpu_set_x", "spmv_mgpu_run", "spmv_mgpu_get_y", "spmv_mgpu_get_timing",
     "spmv_mgpu_slice", "spmv_mgpu_destroy", "spmv_mgpu_unique_id", "spmv_mgpu_create_rank",
     "spmv_mgpu_set_x_device", "spmv_mgpu_set_x_device_on", "spmv_mgpu_y_device", "spmv_mgpu_run_pipelined",
+    "spmv_mgpu_run_graph",
 ]
 
 MGPU_GATHER, MGPU_REDUCE, MGPU_ALLGATHER = 0, 1, 2  # include/csr_hw_wrapper.h SPMV_MGPU_*
@@ -179,6 +180,7 @@ class Lib:
             "spmv_mgpu_set_x_device": (ctypes.c_int, [vp, vp]),
             "spmv_mgpu_set_x_device_on": (ctypes.c_int, [vp, vp, vp]),
             "spmv_mgpu_run_pipelined": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+            "spmv_mgpu_run_graph": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
             "spmv_mgpu_y_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp)]),
         }
         for name, (res, args) in sig.items():
@@ -423,6 +425,14 @@ class MultiGpu:
         ms = ctypes.c_double()
         self.lib._ok(self.lib.L.spmv_mgpu_run_pipelined(self.h, int(exchange), int(steps), ctypes.byref(ms)),
                      "spmv_mgpu_run_pipelined")
+        return float(ms.value)
+
+    def run_graph(self, exchange: int = MGPU_ALLGATHER, iters: int = 8) -> float:
+        """`iters` steps (SpMV + exchange) replayed from one hipGraph (one device per handle);
+        ms per step. The all-gather form leaves A^iters x as x."""
+        ms = ctypes.c_double()
+        self.lib._ok(self.lib.L.spmv_mgpu_run_graph(self.h, int(exchange), int(iters), ctypes.byref(ms)),
+                     "spmv_mgpu_run_graph")
         return float(ms.value)
 
     def y_device_ptr(self, exchange: int = MGPU_GATHER) -> int:

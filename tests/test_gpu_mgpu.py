@@ -194,3 +194,41 @@ def test_mgpu_run_pipelined(exchange, steps):
     with pytest.raises(RuntimeError, match="gather or reduce"):
         mg.run_pipelined(spmv_hw.MGPU_ALLGATHER, 2)
     mg.destroy()
+
+
+@pytest.mark.parametrize("iters", [1, 2, 3])
+def test_mgpu_run_graph(iters):
+    """spmv_mgpu_run_graph: kernels + RCCL exchange captured into one hipGraph and replayed (one
+    device per handle: the one-process-per-GPU form). The all-gather iterates x <- A x, so after
+    `iters` steps x = A^iters x0; odd counts swap the buffers, which re-captures on the next call.
+    Gather and reduce repeat y = A x. Checked against the oracle applied step by step."""
+    import torch
+    lib = spmv_hw.load(np.float64)
+    n, z = 200_000, 3_200_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    mg = spmv_hw.MultiGpu.rank(lib, 0, 1, spmv_hw.mgpu_unique_id(lib), 0, [0, n], n, plan)
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref1 = oracle.spmv_gold(r, c, h[2], h[3])
+    for ex in (spmv_hw.MGPU_GATHER, spmv_hw.MGPU_REDUCE):
+        mg.set_x_device(x)
+        for _ in range(2):  # capture, then replay
+            assert mg.run_graph(ex, iters) > 0
+            assert oracle.scaled_error(r, c, h[2], h[3], ref1, mg.y(ex)) <= 1e-12
+    for rep in range(2):  # second round: re-captured (odd) or replayed (even) from A^iters x0
+        if rep == 0:
+            mg.set_x_device(x)
+            xs = h[3]
+        mg.run_graph(spmv_hw.MGPU_ALLGATHER, iters)
+        ref = xs
+        for _ in range(iters):
+            prev = ref
+            ref = oracle.spmv_gold(r, c, h[2], prev)
+        got = mg.y(spmv_hw.MGPU_ALLGATHER)
+        assert oracle.scaled_error(r, c, h[2], prev, ref, got) <= 1e-12
+        xs = got
+    torch.cuda.synchronize()
+    mg.destroy()
+    plan.destroy()
