@@ -56,3 +56,16 @@ def test_dropin_main_runs_with_compile_time_units(name, exe, ngpus, units):
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("storage_overhead over")][0]
     assert f"{units} non-null handles" in line, line
     assert float(line.split(": ")[1].split(" MB")[0]) > 0
+
+
+@pytest.mark.parametrize("name", ["small", "small_empty", "wide", "longrow"])
+@pytest.mark.parametrize("merge", ["gather", "reduce"])
+def test_run_elf_rccl_merge_passes(name, merge):
+    """The restated main.cpp flow with spmv_hw's RCCL merge forced (one unit on the box's GPU; the
+    same branch takes one unit per GPU on a multi-GPU node): "Verification PASSED!"."""
+    out = subprocess.run([os.path.join(ELF, "run.elf"), os.path.join(GOLDEN, f"{name}.mtx")], capture_output=True,
+                         text=True, timeout=120, env=dict(os.environ, SPMV_NGPUS="1", SPMV_HW_MERGE=merge,
+                                                          SPMV_HW_TRACE="1"))
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "Verification PASSED!" in out.stdout
+    assert "RCCL merge" in out.stderr
