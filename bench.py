@@ -705,6 +705,7 @@ def main():
             key = f"{desc['workload']}_{args.dtype}"
             if (key in tr and tr[key].get("nnz") == nnz_local
                     and tr[key].get("kernel", "").split("<")[0] == kname
+                    and tr[key].get("format", st["format"]) == st["format"]  # same entry layout
                     and (kname != "k_spmv_tiles"  # template arg CB: bytes per stored column
                          or tr[key]["kernel"].endswith(
                              ", %d>" % (1 if st["format"] & 8 else 2 if st["format"] & 1 else 4)))):
