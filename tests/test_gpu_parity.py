@@ -1149,3 +1149,46 @@ def test_sweep_delta_gap_edges(torch, monkeypatch, dtype):
         torch.cuda.synchronize()
         check(row_ptr, col, val, x, ref, y.cpu().numpy(), dtype)
     plan.destroy()
+
+
+@pytest.mark.parametrize("setting", ["threads512", "threads256", "acc32"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sweep_workgroup_and_accumulator_settings(torch, monkeypatch, dtype, setting):
+    """The sweep's other product settings: SPMV_SWEEP_THREADS=512/256 (half / quarter-size panels
+    per workgroup; packed chunks delta-coded, or the unpacked form when the smaller panels make
+    chunk spans too wide) and, for fp32, SPMV_SWEEP_ACC=32 (an fp32 LDS accumulator through
+    compare-and-swap, up to 40,895-row panels; delta-coded only while the panels stay below
+    32,768 rows). y matches the oracle: fp64-accumulating settings within the tight bound of the
+    fp64-accumulated reference, the fp32 accumulator within the north-star 1e-4 of spmv_gold."""
+    if setting == "acc32" and dtype == np.float64:
+        pytest.skip("SPMV_SWEEP_ACC=32 applies to fp32 matrices only")
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    if setting.startswith("threads"):
+        monkeypatch.setenv("SPMV_SWEEP_THREADS", setting[7:])
+    else:
+        monkeypatch.setenv("SPMV_SWEEP_ACC", "32")
+    lib = spmv_hw.load(dtype)
+    n, m, z = 600_000, 3_000_000, 9_600_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, z, seed=12)
+    x = spmv_hw.gen_vector(lib, m, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, m)
+    st = plan.stats()
+    assert st["kernel"] == 2, st
+    if st["format"] & 2 and st["nr_nonempty_rows"] and setting != "acc32":
+        # packed chunks carry delta-coded columns (quarter-size panels of 256-thread workgroups
+        # are sparse enough for chunk spans >= 65536, i.e. the unpacked 14-byte form)
+        assert st["format"] & 64, st
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    plan.destroy()
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    yy = y.cpu().numpy()
+    assert not np.isnan(yy).any()
+    if setting == "acc32":
+        ref = oracle.spmv_gold(row_ptr, c, v, xx)
+        assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TOL[np.dtype(dtype)]
+    else:
+        ref = oracle.spmv_fp64acc(row_ptr, c, v, xx) if dtype == np.float32 else oracle.spmv_gold(row_ptr, c, v, xx)
+        assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(dtype)]
