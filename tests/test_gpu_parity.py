@@ -1192,3 +1192,38 @@ def test_sweep_workgroup_and_accumulator_settings(torch, monkeypatch, dtype, set
     else:
         ref = oracle.spmv_fp64acc(row_ptr, c, v, xx) if dtype == np.float32 else oracle.spmv_gold(row_ptr, c, v, xx)
         assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(dtype)]
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("knob", ["tile_xcd", "sweep_no_lane_order"])
+def test_measurement_layout_switches(torch, monkeypatch, dtype, knob):
+    """Two layout switches kept for measurements: SPMV_TILE_XCD=1 (the tiles
+    dealt XCD-contiguously) on a banded matrix, and SPMV_SWEEP_LANE_ORDER=0 (packed sweep chunks in
+    plain column order, hence no delta-coded columns) on a power-law one. y matches the oracle."""
+    lib = spmv_hw.load(dtype)
+    if knob == "tile_xcd":
+        monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
+        monkeypatch.setenv("SPMV_TILE_XCD", "1")
+        n = 1_000_000
+        rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
+        m = n
+    else:
+        monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+        monkeypatch.setenv("SPMV_SWEEP_LANE_ORDER", "0")
+        n, m = 2_000_000, 10_000_000
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, 16 * n, seed=13)
+    x = spmv_hw.gen_vector(lib, m, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, m)
+    st = plan.stats()
+    if knob == "sweep_no_lane_order":
+        assert st["kernel"] == 2 and st["format"] & 2 and not st["format"] & (4 | 64), st
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    plan.destroy()
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref = oracle.spmv_fp64acc(row_ptr, c, v, xx) if dtype == np.float32 else oracle.spmv_gold(row_ptr, c, v, xx)
+    yy = y.cpu().numpy()
+    assert not np.isnan(yy).any()
+    assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(dtype)]
