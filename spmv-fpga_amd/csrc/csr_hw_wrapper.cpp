@@ -11,6 +11,7 @@
 #include <sys/mman.h>
 #include <sys/time.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -60,6 +61,30 @@ int unit_device(int unit) { return unit % device_count(); }
 // how spmv_hw merges the unit slices (env SPMV_HW_MERGE, read by create_csr_hw_matrix)
 enum { kMergeHost = 0, kMergeGather = 1, kMergeReduce = 2 };
 
+// completion events of the pieces of one y copy (device-to-host), created on first use on the
+// device whose stream records them
+struct d2h_events {
+    int device = 0;
+    std::vector<hipEvent_t> ev;
+    hipEvent_t get(size_t k)
+    {
+        while (ev.size() <= k) {
+            hipEvent_t e = nullptr;
+            check(hipSetDevice(device), "hipSetDevice");
+            const char *bs = std::getenv("SPMV_HW_BLOCKING_SYNC");
+            check(hipEventCreateWithFlags(&e, hipEventDisableTiming | (bs && bs[0] == '1' ? hipEventBlockingSync : 0)),
+                  "hipEventCreate");
+            ev.push_back(e);
+        }
+        return ev[k];
+    }
+    ~d2h_events()
+    {
+        for (hipEvent_t e : ev)
+            (void)hipEventDestroy(e);
+    }
+};
+
 // the RCCL clique of a matrix whose units sit on distinct GPUs (owned by unit 0's handle)
 struct hw_clique {
     spmv_mgpu *mg = nullptr;
@@ -67,6 +92,7 @@ struct hw_clique {
     std::vector<int> devices;       // of units 0..n-1
     ValueType *h_full = nullptr;    // pinned staging of the whole y
     uint64_t rows = 0;
+    d2h_events done;                // of the y copy's pieces (device 0)
     ~hw_clique()
     {
         if (mg)
@@ -86,6 +112,7 @@ struct hw_matrix_impl {
     // staging copy (the reference allocates its y per call, csr_hw_wrapper.cpp:198,287)
     ValueType *d_y = nullptr;
     ValueType *h_stage = nullptr;
+    d2h_events done;  // of the y copy's pieces
     BusDataType *sub[1] = {nullptr};
     IndexType nr_rows[1] = {0}, nr_cols[1] = {0}, nr_nzeros[1] = {0}, nr_ci[1] = {0}, nr_val[1] = {0};
 };
@@ -176,38 +203,101 @@ int merge_mode(int units)
     return m;
 }
 
-// adds parts[k].src into parts[k].dst on up to 16 host threads; each thread maps its part of the
-// caller's y writable first (prefault, while the DMA runs), then waits until wait_dma() returned
+int env_pieces(int dflt)
+{
+    const char *e = std::getenv("SPMV_HW_PIECES");
+    return e ? std::max(1, std::atoi(e)) : dflt;
+}
+
+// one piece of accum_results' '+=': dst[i] += src[i] once `ready` (the copy of src) completed
 struct add_part {
     ValueType *dst;
     const ValueType *src;
     uint64_t count;
+    hipEvent_t ready;
 };
-template <typename WaitDma>
-void host_accumulate(const std::vector<add_part> &parts, WaitDma wait_dma)
+
+// Copies rows [0, rows) of a device y slice into pinned staging on stream s as `pieces` copies,
+// each followed by an event, and appends one add_part per piece (dst = the caller's y). The
+// host adds of a piece then start while later pieces are still crossing PCIe. 8 pieces of y in
+// all by default (env SPMV_HW_PIECES); SPMV_HW_PIPELINE=0: one copy and one event for the whole
+// slice (every add waits for all of it). Measured on 10M fp64 rows, one GPU
+// (profiles/r03aq_spmv_hw_merge.jsonl): accumulation 1.86-1.91 ms pieced vs 2.71-2.93 ms whole,
+// against 1.43 ms for the bare copy.
+void enqueue_d2h(ValueType *y_dst, ValueType *stage, const ValueType *d_src, uint64_t rows, uint64_t pieces,
+                 hipStream_t s, d2h_events &done, std::vector<add_part> &parts)
 {
-    std::atomic<bool> landed{false};
+    const char *pe = std::getenv("SPMV_HW_PIPELINE");
+    const bool pipe = !(pe && pe[0] == '0');
+    if (!pipe) {
+        check(hipMemcpyAsync(stage, d_src, rows * sizeof(ValueType), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(y)");
+        check(hipEventRecord(done.get(0), s), "hipEventRecord");
+    }
+    for (uint64_t t = 0; t < pieces; ++t) {
+        const uint64_t b = rows * t / pieces, e = rows * (t + 1) / pieces;
+        if (pipe) {
+            check(hipMemcpyAsync(stage + b, d_src + b, (e - b) * sizeof(ValueType), hipMemcpyDeviceToHost, s),
+                  "hipMemcpyAsync(y)");
+            check(hipEventRecord(done.get(t), s), "hipEventRecord");
+        }
+        parts.push_back({y_dst + b, stage + b, e - b, done.get(pipe ? t : 0)});
+    }
+}
+
+// adds the parts in on up to 16 host threads, in copy order: thread t adds the t-th sixteenth of
+// every part as soon as that part's copy has landed, so the adds run behind the DMA and the last
+// piece to land leaves 1/16 of a piece per thread (env SPMV_HW_ADD_SPLIT=0: thread t adds whole
+// parts t, t + 16, ... instead). Each thread first maps its ranges of the caller's y writable
+// (prefault, while the DMA runs). Returns when (timestamp_us) the last copy was seen complete.
+double host_accumulate(const std::vector<add_part> &parts)
+{
     const char *pf_env = std::getenv("SPMV_HW_PREFAULT");
     const bool pf = !(pf_env && pf_env[0] == '0');  // 0: let the adds take the page faults
-    auto work = [&](const add_part &q, bool wait) {
+    const char *se = std::getenv("SPMV_HW_ADD_SPLIT");
+    const bool split = !(se && se[0] == '0');
+    const char *te = std::getenv("SPMV_HW_ADD_THREADS");
+    uint64_t total = 0;
+    for (const add_part &q : parts)
+        total += q.count;
+    const size_t T = parts.empty() ? 0
+                     : total < (1u << 18) ? 1
+                     : std::min<size_t>(te ? std::max(1, std::atoi(te)) : 16, split ? size_t(64) : parts.size());
+    // thread t's range of part k: [b, e)
+    auto range = [&](size_t t, size_t k, uint64_t &b, uint64_t &e) {
+        const uint64_t n = parts[k].count;
+        if (split)
+            b = n * t / T, e = n * (t + 1) / T;
+        else
+            b = 0, e = k % T == t ? n : 0;
+    };
+    std::vector<double> landed(T, 0.0);
+    auto work = [&](size_t t) {
+        uint64_t b, e;
         if (pf)
-            prefault(q.dst, q.count);
-        while (wait && !landed.load(std::memory_order_acquire))
-            std::this_thread::yield();
-        for (uint64_t i = 0; i < q.count; ++i)
-            q.dst[i] += q.src[i];
+            for (size_t k = 0; k < parts.size(); ++k) {
+                range(t, k, b, e);
+                if (e > b)
+                    prefault(parts[k].dst + b, e - b);
+            }
+        for (size_t k = 0; k < parts.size(); ++k) {
+            range(t, k, b, e);
+            if (e <= b)
+                continue;
+            const add_part &q = parts[k];
+            check(hipEventSynchronize(q.ready), "y copy");
+            landed[t] = timestamp_us();
+            for (uint64_t i = b; i < e; ++i)
+                q.dst[i] += q.src[i];
+        }
     };
     std::vector<std::thread> th;
-    for (size_t k = 1; k < parts.size(); ++k)
-        th.emplace_back(work, std::cref(parts[k]), true);
-    if (pf && !parts.empty())
-        prefault(parts[0].dst, parts[0].count);
-    wait_dma();
-    landed.store(true, std::memory_order_release);
-    if (!parts.empty())
-        work(parts[0], false);
+    for (size_t t = 1; t < T; ++t)
+        th.emplace_back(work, t);
+    if (T)
+        work(0);
     for (auto &t : th)
         t.join();
+    return T ? *std::max_element(landed.begin(), landed.end()) : timestamp_us();
 }
 
 }  // namespace
@@ -458,17 +548,14 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         // one D2H copy of the whole y from GPU 0, then the host += (accum_results into y_fpga)
         const double ra_s = timestamp_us();
         check(hipSetDevice(c->devices[0]), "hipSetDevice");
-        const hipStream_t s0 = unit_stream(0);
-        if (c->rows)
-            check(hipMemcpyAsync(c->h_full, mgpu_root_y(c->mg), c->rows * sizeof(ValueType), hipMemcpyDeviceToHost, s0),
-                  "hipMemcpyAsync(y)");
         std::vector<add_part> parts;
-        const uint64_t T = c->rows < (1u << 18) ? 1 : 16;
-        for (uint64_t t = 0; t < T && c->rows; ++t) {
-            const uint64_t b = c->rows * t / T, e = c->rows * (t + 1) / T;
-            parts.push_back({y_fpga->values + b, c->h_full + b, e - b});
-        }
-        host_accumulate(parts, [&] { check(hipStreamSynchronize(s0), "y copy"); });
+        c->done.device = c->devices[0];
+        if (c->rows)
+            enqueue_d2h(y_fpga->values, c->h_full, mgpu_root_y(c->mg), c->rows, c->rows < (1u << 18) ? 1 : env_pieces(8),
+                        unit_stream(0), c->done, parts);
+        const double landed = host_accumulate(parts);
+        if (trace)
+            std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "spmv_hw: D2H landed", (landed - ra_s) / 1000);
         tr("spmv_hw: D2H + host accumulation", ra_s);
         const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
         std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
@@ -494,39 +581,35 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
     std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
 
     // accum_results: every unit's slice comes back over its own PCIe link into pinned memory
-    // (all copies in flight together). Host threads map their part of y_fpga while the DMA
-    // runs, then add the staged slices in once every copy has landed
+    // (all copies in flight together, each cut into pieces); host threads map their part of
+    // y_fpga while the DMA runs and add each piece in as soon as its copy has landed
     const double ra_s = timestamp_us();
-    for (int u = 0; u < units; ++u) {
-        hw_matrix_impl *m = impl(hw_matrix[u]);
-        const IndexType rows = m->row_end - m->row_begin;
-        if (!rows)
-            continue;
-        check(hipSetDevice(m->device), "hipSetDevice");
-        check(hipMemcpyAsync(m->h_stage, m->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost,
-                             unit_stream(u)),
-              "hipMemcpyAsync(y)");
-    }
-    tr("spmv_hw: D2H enqueue", ra_s);
-    std::vector<add_part> parts;  // up to 8 per unit, 16 in total
+    // pieces in landing order: piece j of every unit (their copies run in parallel), then j + 1
+    std::vector<std::vector<add_part>> per_unit(units);
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
         const uint64_t rows = m->row_end - m->row_begin;
-        const uint64_t T = rows < (1u << 18) ? 1 : std::min(8, std::max(1, 16 / units));
-        for (uint64_t t = 0; t < T && rows; ++t) {
-            const uint64_t b = rows * t / T, e = rows * (t + 1) / T;
-            parts.push_back({y_fpga->values + m->row_begin + b, m->h_stage + b, e - b});
-        }
+        if (!rows)
+            continue;
+        check(hipSetDevice(m->device), "hipSetDevice");
+        m->done.device = m->device;
+        enqueue_d2h(y_fpga->values + m->row_begin, m->h_stage, m->d_y, rows,
+                    rows < (1u << 18) ? 1 : std::max(2, env_pieces(8) / units), unit_stream(u), m->done,
+                    per_unit[u]);
     }
-    host_accumulate(parts, [&] {
-        for (int u = 0; u < units; ++u) {
-            if (impl(hw_matrix[u])->row_end == impl(hw_matrix[u])->row_begin)
-                continue;
-            check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
-            check(hipStreamSynchronize(unit_stream(u)), "y copy");
-        }
-        tr("spmv_hw: D2H done", ra_s);
-    });
+    std::vector<add_part> parts;
+    for (size_t j = 0, more = 1; more; ++j) {
+        more = 0;
+        for (int u = 0; u < units; ++u)
+            if (j < per_unit[u].size()) {
+                parts.push_back(per_unit[u][j]);
+                more = 1;
+            }
+    }
+    tr("spmv_hw: D2H enqueue", ra_s);
+    const double landed = host_accumulate(parts);
+    if (trace)
+        std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "spmv_hw: D2H landed", (landed - ra_s) / 1000);
     tr("spmv_hw: host accumulation", ra_s);
     const double ra_exec = (timestamp_us() - ra_s) / 1000.0;
     std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);

@@ -67,13 +67,16 @@ def test_rccl_merge_on_golden_fixtures(monkeypatch, capfd, merge, name, dtype, t
     assert "RCCL merge" in err  # the trace names the branch that ran
 
 
+@pytest.mark.parametrize("pipeline", ["1", "0"])
 @pytest.mark.parametrize("merge", ["gather", "reduce", "host"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_rccl_merge_powerlaw(monkeypatch, capfd, merge, dtype):
+def test_rccl_merge_powerlaw(monkeypatch, capfd, merge, dtype, pipeline):
     """A 1M-row power-law matrix (sweep / binned plans) through each merge; host is the PCIe
-    merge the RCCL branch replaces."""
+    merge the RCCL branch replaces. pipeline 1 (default): y comes back in 64 pieces, each added
+    in as soon as it landed; 0: one copy, every add after it (SPMV_HW_PIPELINE)."""
     monkeypatch.setenv("SPMV_NGPUS", str(_ndev()))
     monkeypatch.setenv("SPMV_HW_MERGE", merge)
+    monkeypatch.setenv("SPMV_HW_PIPELINE", pipeline)
     monkeypatch.setenv("SPMV_HW_TRACE", "1")
     lib = spmv_hw.load(dtype)
     n, z = 1_000_000, 16_000_000
