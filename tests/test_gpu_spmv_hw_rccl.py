@@ -121,3 +121,24 @@ def test_auto_merge_keeps_host_for_shared_gpus(monkeypatch, capfd):
     assert oracle.scaled_error(row_ptr, col, val, x, y_gold, y) <= 1e-12
     _, err = capfd.readouterr()
     assert "RCCL merge" not in err
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_host_merge_pieces_of_several_units(monkeypatch, split):
+    """The host merge with 3 units (virtual CUs on the box's GPU) of a 1M-row power-law matrix:
+    every unit's slice comes back in pieces, the pieces are added in landing order (piece j of
+    every unit, then j + 1) by 16 threads, each taking a sixteenth of every piece (split 1) or
+    whole pieces (split 0); y matches the oracle and a second call adds A*x once more."""
+    monkeypatch.setenv("SPMV_NGPUS", str(_ndev() + 2))
+    monkeypatch.setenv("SPMV_HW_MERGE", "host")
+    monkeypatch.setenv("SPMV_HW_ADD_SPLIT", split)
+    lib = spmv_hw.load(np.float64)
+    n, z = 1_000_000, 16_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=9)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    h_rp, h_col = rp.cpu().numpy().view(np.uint32), col.cpu().numpy().view(np.uint32)
+    h_val, h_x = val.cpu().numpy(), x.cpu().numpy()
+    y1, y2 = _flow(lib, h_rp, h_col, h_val, h_x, n, np.float64, calls=2)
+    ref = oracle.spmv_gold(h_rp, h_col, h_val, h_x)
+    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y1) <= 1e-12
+    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y2 - y1) <= 1e-12
