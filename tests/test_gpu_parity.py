@@ -607,6 +607,21 @@ def test_sweep_fused_combine_bitwise_equals_combine_kernel(torch, monkeypatch):
     ref = oracle.spmv_gold(row_ptr, c, v, xx)
     for _, y in ys.values():
         check(row_ptr, c, v, xx, ref, y, np.float64)
+    # the default (non-deterministic) sweep with the fused combine, 4 and 8 pieces
+    monkeypatch.delenv("SPMV_SWEEP_DETERMINISTIC")
+    monkeypatch.setenv("SPMV_SWEEP_COMBINE", "fused")
+    for pieces in ("", "8"):
+        if pieces:
+            monkeypatch.setenv("SPMV_SWEEP_PIECES", pieces)
+        else:
+            monkeypatch.delenv("SPMV_SWEEP_PIECES", raising=False)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n_full)
+        for _ in range(3):
+            y = torch.full((r1 - r0,), float("nan"), dtype=x.dtype, device="cuda")
+            plan.run(x, y)
+            torch.cuda.synchronize()
+            check(row_ptr, c, v, xx, ref, y.cpu().numpy(), np.float64)
+        plan.destroy()
 
 
 # ---- gold order: bitwise the reference's spmv_gold (csr.cpp:184-194) ----
