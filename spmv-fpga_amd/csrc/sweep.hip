@@ -285,6 +285,30 @@ __global__ __launch_bounds__(T) void k_spmv_sweep(
 // prefix sum turns the deltas into columns. A chunk with a gap above 511 (~1 in 10^5 on the
 // headline matrix) has bit 31 of dbase set and its absolute columns in `side` (uniform branch).
 // `rc` is not read (a delta plan frees its 12-byte words).
+#ifdef SPMV_ABLATIONS
+// measurement build only: per workgroup of the last k_spmv_sweep_packed launch, the 100 MHz
+// real-time clock at its start, at the end of its sweep and after its y / partial store, and its
+// XCC and HW_ID registers (tools/wg_timeline.py reads them with spmv_abl_wg_times)
+__device__ unsigned long long g_abl_wg[4 * 4096];
+#define ABL_WG_STAMP(k)                                                                            \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                                 \
+            g_abl_wg[4 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+#define ABL_WG_IDS()                                                                               \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                                 \
+            g_abl_wg[4 * blockIdx.x + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) | \
+                                           (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    \
+    } while (0)
+#else
+#define ABL_WG_STAMP(k) \
+    do {                \
+    } while (0)
+#define ABL_WG_IDS() \
+    do {             \
+    } while (0)
+#endif
 template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double, bool DL = false>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
@@ -304,6 +328,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     __shared__ uint32_t progress[T / 64];
+    ABL_WG_STAMP(0);
+    ABL_WG_IDS();
     for (uint32_t i = threadIdx.x; i <= R; i += T)
         ylds[i] = A(0);
     if (threadIdx.x < T / 64)
@@ -457,7 +483,9 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     if constexpr (ABL == 8 || ABL == 9)
         lds_add(&ylds[R], sink);
     __syncthreads();
+    ABL_WG_STAMP(1);
     write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
+    ABL_WG_STAMP(2);
 }
 
 // Deterministic form (env SPMV_SWEEP_DETERMINISTIC=1): the same plan, layout and gathers as
@@ -1365,3 +1393,13 @@ int probe_locality(const IndexType *d_rp, const IndexType *d_col, IndexType n, h
 }
 
 }  // namespace spmvhw
+
+#ifdef SPMV_ABLATIONS
+// measurement build only: copies n words of the workgroup timeline (4 per workgroup) to the host
+extern "C" int spmv_abl_wg_times(unsigned long long *out, unsigned n)
+{
+    if (!out || n > 4 * 4096)
+        return 1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(spmvhw::g_abl_wg), size_t(n) * 8, 0, hipMemcpyDeviceToHost) != hipSuccess;
+}
+#endif

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Workgroup timeline of one k_spmv_sweep_packed launch (measurement build, SPMV_HW_ABLATIONS=1):
+where the time of a strong-scaling slice goes (the N = 8 slice costs ~5.6 ps per
+non-zero against 4.8 in the whole matrix).
+
+For each workgroup the kernel records the 100 MHz real-time clock at its start, at the end of its
+sweep and after its y / partial-sum store, plus its XCC id. After a few warm runs of the plan this
+prints, for the last launch: the start spread (dispatch ramp), the distribution of sweep end times
+(the tail: how long the first-finished CUs sit idle), the store phase, and per-XCC means. One JSON
+line per matrix. Rows [r0, r1) of the 10M/160M power-law matrix (--slice k/N: slice k of N).
+Measurement tool, not product code."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+os.environ["SPMV_HW_ABLATIONS"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "spmv-fpga_amd"))
+import torch  # noqa: E402
+
+import spmv_hw  # noqa: E402
+
+
+def pct(a, q):
+    return round(float(np.percentile(a, q)), 2)
+
+
+def timeline(lib, plan, x, y, units):
+    for _ in range(5):
+        plan.run(x, y)
+    torch.cuda.synchronize()
+    n = 4 * min(units, 4096)
+    buf = (ctypes.c_ulonglong * n)()
+    if lib.L.spmv_abl_wg_times(buf, ctypes.c_uint(n)):
+        raise RuntimeError("spmv_abl_wg_times failed")
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4)
+    t = a[:, :3].astype(np.int64)
+    t0 = t[:, 0].min()
+    us = (t - t0) / 100.0  # 100 MHz ticks -> microseconds
+    xcc = (a[:, 3] >> np.uint64(32)).astype(np.int64)
+    start, sweep_end, done = us[:, 0], us[:, 1], us[:, 2]
+    per_xcc = {int(k): {"n": int((xcc == k).sum()), "sweep_us": round(float((sweep_end - start)[xcc == k].mean()), 2),
+                        "end_us": round(float(done[xcc == k].mean()), 2)} for k in np.unique(xcc)}
+    return {"units": int(units), "start_us": {"p50": pct(start, 50), "max": pct(start, 100)},
+            "sweep_us": {"min": pct(sweep_end - start, 0), "p50": pct(sweep_end - start, 50),
+                         "max": pct(sweep_end - start, 100)},
+            "sweep_end_us": {"min": pct(sweep_end, 0), "p10": pct(sweep_end, 10), "p50": pct(sweep_end, 50),
+                             "p90": pct(sweep_end, 90), "max": pct(sweep_end, 100)},
+            "store_us": {"p50": pct(done - sweep_end, 50), "max": pct(done - sweep_end, 100)},
+            "last_done_us": pct(done, 100),
+            "idle_frac": round(float(1.0 - (done - start).sum() / (len(done) * done.max())), 4),
+            "per_xcc": per_xcc}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slices", default="0/8,0/4,0/1", help="k/N: rows of slice k of N (nnz-balanced)")
+    a = ap.parse_args()
+    lib = spmv_hw.load(np.float64)
+    n, z = 10_000_000, 160_000_000
+    rp_full, _ = lib.powerlaw_row_ptr(n, z, n, 4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    for sl in a.slices.split(","):
+        k, N = (int(v) for v in sl.split("/"))
+        cuts = np.searchsorted(rp_full, [z * i // N for i in range(N + 1)])
+        cuts[0], cuts[-1] = 0, n
+        r0, r1 = int(cuts[k]), int(cuts[k + 1])
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4, row_begin=r0, row_end=r1)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+        st = plan.stats()
+        y = torch.empty(r1 - r0, dtype=torch.float64, device="cuda")
+        out = {"slice": sl, "rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "format": st["format"]}
+        if st["kernel"] == 2:
+            out.update(timeline(lib, plan, x, y, st["nr_tiles"]))
+        print(json.dumps(out), flush=True)
+        plan.destroy()
+        del rp, col, val, y
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
