@@ -1088,6 +1088,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         if (hipGetDeviceProperties(&prop, p.device) == hipSuccess && prop.multiProcessorCount > 0)
             cus = prop.multiProcessorCount;
     }
+    const int chip_cus = cus;
     cus *= 1024 / p.sweep_threads;  // resident workgroups per round
     // env SPMV_SWEEP_SPLIT: 0 = never split, 2 = split whenever >= 2 pieces fit, else heuristic
     const char *senv = std::getenv("SPMV_SWEEP_SPLIT");
@@ -1097,6 +1098,20 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     const bool allow_split = !(senv && senv[0] == '0');
     const bool force_split = senv && senv[0] == '2';
     bool split_mode = false;
+    // XCC bias: the units the round-robin dispatch sends to even XCCs (unit % 8 even; block b
+    // runs on XCC b % 8 in every launch probed, tools/xcc_map_probe.py) get (1 - d) x the mean
+    // entries, the odd ones (1 + d) x; weight of the units [0, u): u - d * (u & 1). Why: on the
+    // MI355X boxes measured, workgroups on even XCCs sweep 2-4 % slower than on odd ones, in the
+    // whole matrix and in the strong-scaling slices (tools/wg_timeline.py,
+    // profiles/r03ay_wg_timeline.jsonl, two boxes), and the launch ends with the slowest XCC.
+    // Defaults on a whole chip (256 CUs = 8 XCDs): d = 0.015 for whole panels, 0.02 for split
+    // pieces (interleaved A/B, profiles/r03bb_xcc_bias.jsonl: 10M/160M -1.3 %, the N = 8 slice
+    // -2.0 %, N = 4 -0.7 %); env SPMV_SWEEP_XCC_BIAS=d overrides both (0 = even cut).
+    const char *xbenv = std::getenv("SPMV_SWEEP_XCC_BIAS");
+    double xbias_split = xbenv ? std::atof(xbenv) : chip_cus == 256 ? 0.02 : 0.0;
+    double xbias = xbenv ? std::atof(xbenv) : chip_cus == 256 ? 0.015 : 0.0;
+    if (!(xbias > -0.5 && xbias < 0.5))
+        xbias = xbias_split = 0.0;
     std::vector<uint32_t> prow;
     for (uint64_t P = std::max<uint64_t>(1, (n + rmax - 1) / rmax);; ++P) {
         {
@@ -1116,9 +1131,14 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         bool ok = true;
         IndexType r = 0;
         for (uint64_t q = 1; q <= P && ok; ++q) {
-            const uint64_t target = nnz * q / P;
+            const uint64_t target =
+                split_mode || xbias == 0.0
+                    ? nnz * q / P
+                    : (uint64_t)(double(nnz) * (double(q) - xbias * double(q & 1)) / (double(P) - xbias * double(P & 1)));
             IndexType e = (q == P) ? n : (IndexType)(std::lower_bound(h_rp, h_rp + n + 1, (IndexType)target) - h_rp);
             e = std::max(e, r);
+            if (e - r > rmax && xbias != 0.0 && !split_mode && q < P)
+                e = r + rmax;  // a biased cut past the LDS rows: this panel takes what fits
             if (e - r > rmax)
                 ok = false;
             prow.push_back(e);
@@ -1126,12 +1146,19 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         }
         if (ok)
             break;
+        if (xbias != 0.0 && !split_mode) {  // the biased cut overflows a panel: cut evenly
+            xbias = 0.0;
+            --P;
+            continue;
+        }
         if (P >= n) {
             set_error("build_sweep: cannot form panels");
             return 1;
         }
     }
     const uint32_t P = (uint32_t)(prow.size() - 1);
+    if (split_mode)
+        xbias = xbias_split;  // the pieces' cut below (the panels were cut evenly)
     const std::vector<uint32_t> &srow = prow;  // sort segments = the panels
     const uint32_t S = (uint32_t)(srow.size() - 1);
     std::vector<uint32_t> off(S + 1), poff(S + 1);
@@ -1178,9 +1205,14 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
         const uint32_t k = punit[q + 1] - punit[q];
         multi |= k > 1;
+        const uint32_t u0 = punit[q];
+        auto wc = [&](uint32_t u) { return double(u) - xbias * double(u & 1); };  // weight of units [0, u)
         for (uint32_t t = 0; t < k; ++t) {
-            uent[punit[q] + t] = (uint32_t)(poff[q] + kSweepChunk * (chunks * t / k));
-            upanel[punit[q] + t] = q;
+            const uint64_t c = split_mode && xbias != 0.0
+                                   ? (uint64_t)(double(chunks) * (wc(u0 + t) - wc(u0)) / (wc(u0 + k) - wc(u0)))
+                                   : chunks * t / k;
+            uent[u0 + t] = (uint32_t)(poff[q] + kSweepChunk * c);
+            upanel[u0 + t] = q;
         }
     }
     uent[U] = poff[P];
