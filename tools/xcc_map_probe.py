@@ -1,3 +1,9 @@
+#!/usr/bin/env python3
+"""Which XCC runs sweep workgroup b? (measurement build, SPMV_HW_ABLATIONS=1.) For 40 launches of a
+2M-row and of the 10M-row power-law sweep plan, reads each workgroup's HW_REG_XCC_ID (stamped by
+k_spmv_sweep_packed, see tools/wg_timeline.py) and prints the set of (xcc - b) mod 8 per launch: a
+single 0 means block b ran on XCC b % 8, the assumption of the sweep's XCC bias.
+Measurement tool, not product code."""
 import ctypes, os, sys, json
 os.environ["SPMV_HW_ABLATIONS"] = "1"
 sys.path.insert(0, "spmv-fpga_amd")
