@@ -1242,3 +1242,40 @@ def test_measurement_layout_switches(torch, monkeypatch, dtype, knob):
     yy = y.cpu().numpy()
     assert not np.isnan(yy).any()
     assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(dtype)]
+
+
+@pytest.mark.parametrize("bias", ["0", "0.1", "default"])
+@pytest.mark.parametrize("shape", ["panels", "pieces", "full"])
+def test_sweep_xcc_bias(torch, monkeypatch, shape, bias):
+    """The sweep's XCC bias: units that run on even XCCs cut lighter than odd ones.
+    'panels': 2M x 2M / 32M, whole panels (the biased panel cut); 'pieces': an N = 8-like slice,
+    1.25M x 10M / 20M, split pieces (the biased piece cut); 'full': the 10M/160M matrix, whose
+    panels sit within 5 % of the LDS row cap, so a 10 % bias clamps panels at the cap and then
+    falls back to the even cut. The unit count never changes, and y matches the oracle."""
+    if shape == "full" and bias != "0.1":
+        pytest.skip("the full matrix with the default cut runs in test_gpu_fullsize.py")
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    if bias == "default":
+        monkeypatch.delenv("SPMV_SWEEP_XCC_BIAS", raising=False)
+    else:
+        monkeypatch.setenv("SPMV_SWEEP_XCC_BIAS", bias)
+    lib = spmv_hw.load(np.float64)
+    n, m, z = {"panels": (2_000_000, 2_000_000, 32_000_000), "pieces": (1_250_000, 10_000_000, 20_000_000),
+               "full": (10_000_000, 10_000_000, 160_000_000)}[shape]
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, z, seed=4)
+    x = spmv_hw.gen_vector(lib, m, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, m)
+    st = plan.stats()
+    assert st["kernel"] == 2, st
+    assert st["nr_tiles"] == {"panels": 256, "pieces": 252, "full": 512}[shape], st
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    plan.destroy()
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    del rp, col, val
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    yy = y.cpu().numpy()
+    assert not np.isnan(yy).any()
+    ref = oracle.spmv_gold(row_ptr, c, v, xx)
+    assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(np.float64)]
