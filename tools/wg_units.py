@@ -2,8 +2,8 @@
 """Per-unit sweep times of the 10M/160M plan over several launches (measurement build): are the
 slow units the same panels every launch (a property of the panel: rows, longest row) or the
 same CUs (a property of the hardware)? Prints one JSON line: per launch the Pearson correlation of
-unit times with launch 0, and the correlation of unit time with the panel's row count and longest
-row. Measurement tool, not product code."""
+unit times with launch 0, the share of units on the same CU (HW_ID) as in launch 0, and the
+per-unit mean times. Measurement tool, not product code."""
 import ctypes
 import json
 import os
@@ -40,22 +40,11 @@ def main():
             hw.append(a[:, 3])
     T = np.array(times)
     mean = T.mean(axis=0)
-    # panel features from the row pointer (the plan's panels are its units here: no split)
-    h_rp = rp.cpu().numpy().view(np.uint32).astype(np.int64)
-    lens = np.diff(h_rp)
-    # reconstruct nnz-balanced, XCC-biased cuts is not needed: use the plan's own panel rows
-    prow = (ctypes.c_uint32 * (U + 1))()
-    feats = {}
-    if hasattr(lib.L, "spmv_plan_panel_rows") and lib.L.spmv_plan_panel_rows(plan.h, prow, ctypes.c_uint(U + 1)) == 0:
-        pr = np.frombuffer(prow, dtype=np.uint32).astype(np.int64)
-        rows = np.diff(pr)
-        longest = np.array([lens[pr[i]:pr[i + 1]].max() for i in range(U)])
-        feats = {"corr_rows": float(np.corrcoef(mean, rows)[0, 1]), "corr_longest_row": float(np.corrcoef(mean, longest)[0, 1])}
     out = {"units": U, "launches": len(T), "mean_us": round(float(mean.mean()), 2), "spread_us": round(float(mean.max() - mean.min()), 2),
            "corr_with_launch0": [round(float(np.corrcoef(T[0], T[k])[0, 1]), 3) for k in range(len(T))],
            "same_hw_id_as_launch0": [float((hw[0] == hw[k]).mean()) for k in range(len(hw))],
            "round1_vs_round2_corr": round(float(np.corrcoef(mean[:U // 2], mean[U // 2:])[0, 1]), 3) if U % 2 == 0 else None,
-           "per_unit_mean_us": [round(float(v), 1) for v in mean], **feats}
+           "per_unit_mean_us": [round(float(v), 1) for v in mean]}
     print(json.dumps(out), flush=True)
 
 
