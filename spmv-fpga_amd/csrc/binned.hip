@@ -78,6 +78,27 @@ template <int PER> struct BinDelta;
 template <> struct BinDelta<4> { typedef uint32_t T; };
 template <> struct BinDelta<2> { typedef uint16_t T; };
 
+#ifdef SPMV_ABLATIONS
+// measurement build only: per workgroup of the last launch of pass K (0 = k_bin_mul, 1 =
+// k_bin_acc) the 100 MHz real-time clock at its start and after its last store (behind a
+// barrier), and its XCC id (tools/wg_timeline.py --binned reads them with spmv_abl_bin_times)
+__device__ unsigned long long g_abl_bin[2][4 * 4096];
+#define BN_STAMP(K, k)                                                                             \
+    do {                                                                                           \
+        if ((k) == 1)                                                                              \
+            __syncthreads();                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) {                                               \
+            g_abl_bin[K][4 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();                 \
+            if ((k) == 0)                                                                          \
+                g_abl_bin[K][4 * blockIdx.x + 3] = (unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32; \
+        }                                                                                          \
+    } while (0)
+#else
+#define BN_STAMP(K, k) \
+    do {               \
+    } while (0)
+#endif
+
 // Pass 1: unit u = entries [ub[u], ub[u+1]) of window uwin[u] (both multiples of PER).
 // AL: x is 16-byte aligned, so the window is staged with 16-byte loads.
 // POL (variants 3-5, the same y): bit 0 = temporal (default-policy) product stores instead of
@@ -93,6 +114,7 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
     typedef typename BinVec<V>::T VT;
     typedef typename BinVec<V>::I IT;
     constexpr int PER = 16 / sizeof(V);
+    BN_STAMP(0, 0);
     const uint32_t u = blockIdx.x;
     const uint64_t c0 = (uint64_t)uwin[u] * W;
     const uint32_t wn = (uint32_t)std::min<uint64_t>(W, ncols - c0);  // columns of this window
@@ -170,6 +192,7 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
             }
         }
     }
+    BN_STAMP(0, 1);
 }
 
 // Pass 2: workgroup = panel p (rows [panel_row[p], panel_row[p+1])). Wave v takes windows v,
@@ -196,6 +219,7 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
     constexpr int PER = 16 / sizeof(V);
     constexpr uint32_t STEP = 64 * PER;
     constexpr uint32_t WAVES = kBinT / 64;
+    BN_STAMP(1, 0);
     for (uint32_t i = threadIdx.x; i < slots; i += kBinT)
         ys[i] = 0.0;
     __syncthreads();
@@ -311,6 +335,7 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
     const uint32_t r0 = panel_row[p], nr = panel_row[p + 1] - r0;
     for (uint32_t i = threadIdx.x; i < nr; i += kBinT)
         y[r0 + i] = (V)ys[i];
+    BN_STAMP(1, 1);
 }
 
 // row of entry j: the last row r < n with rp[r] <= j (empty rows are skipped over)
@@ -775,3 +800,14 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
 }
 
 }  // namespace spmvhw
+
+#ifdef SPMV_ABLATIONS
+// measurement build only: n words of pass `pass`'s workgroup timeline (4 per workgroup)
+extern "C" int spmv_abl_bin_times(int pass, unsigned long long *out, unsigned n)
+{
+    if (!out || pass < 0 || pass > 1 || n > 4 * 4096)
+        return 1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(spmvhw::g_abl_bin), size_t(n) * 8, size_t(pass) * 4 * 4096 * 8,
+                               hipMemcpyDeviceToHost) != hipSuccess;
+}
+#endif

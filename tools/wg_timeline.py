@@ -8,6 +8,8 @@ sweep and after its y / partial-sum store, plus its XCC id. After a few warm run
 prints, for the last launch: the start spread (dispatch ramp), the distribution of sweep end times
 (the tail: how long the first-finished CUs sit idle), the store phase, and per-XCC means. One JSON
 line per matrix. Rows [r0, r1) of the 10M/160M power-law matrix (--slice k/N: slice k of N).
+--binned: the fp32 10M/160M matrix on the binned kernel, per pass the workgroup durations and
+their even- / odd-XCC means.
 Measurement tool, not product code."""
 import argparse
 import ctypes
@@ -29,15 +31,34 @@ def pct(a, q):
     return round(float(np.percentile(a, q)), 2)
 
 
+def read_stamps(lib, units, binned_pass=None):
+    n = 4 * min(units, 4096)
+    buf = (ctypes.c_ulonglong * n)()
+    rc = (lib.L.spmv_abl_wg_times(buf, ctypes.c_uint(n)) if binned_pass is None
+          else lib.L.spmv_abl_bin_times(ctypes.c_int(binned_pass), buf, ctypes.c_uint(n)))
+    if rc:
+        raise RuntimeError("reading the workgroup stamps failed")
+    return np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).copy()
+
+
+def bin_pass(a):
+    """start / end clocks of one binned pass (slots 0, 1) and the XCC id (slot 3)."""
+    t = a[:, :2].astype(np.int64)
+    us = (t - t[:, 0].min()) / 100.0
+    xcc = (a[:, 3] >> np.uint64(32)).astype(np.int64)
+    dur = us[:, 1] - us[:, 0]
+    return {"units": int(len(a)), "dur_us": {"min": pct(dur, 0), "p50": pct(dur, 50), "max": pct(dur, 100)},
+            "end_us": {"p10": pct(us[:, 1], 10), "p50": pct(us[:, 1], 50), "max": pct(us[:, 1], 100)},
+            "even_xcc_dur_us": round(float(dur[xcc % 2 == 0].mean()), 2),
+            "odd_xcc_dur_us": round(float(dur[xcc % 2 == 1].mean()), 2),
+            "per_xcc_dur_us": {int(k): round(float(dur[xcc == k].mean()), 2) for k in np.unique(xcc)}}
+
+
 def timeline(lib, plan, x, y, units):
     for _ in range(5):
         plan.run(x, y)
     torch.cuda.synchronize()
-    n = 4 * min(units, 4096)
-    buf = (ctypes.c_ulonglong * n)()
-    if lib.L.spmv_abl_wg_times(buf, ctypes.c_uint(n)):
-        raise RuntimeError("spmv_abl_wg_times failed")
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4)
+    a = read_stamps(lib, units)
     t = a[:, :3].astype(np.int64)
     t0 = t[:, 0].min()
     us = (t - t0) / 100.0  # 100 MHz ticks -> microseconds
@@ -59,7 +80,27 @@ def timeline(lib, plan, x, y, units):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--slices", default="0/8,0/4,0/1", help="k/N: rows of slice k of N (nnz-balanced)")
+    ap.add_argument("--binned", action="store_true",
+                    help="the fp32 10M/160M matrix on the binned kernel instead: both passes' timelines")
     a = ap.parse_args()
+    if a.binned:
+        os.environ["SPMV_HW_KERNEL"] = "binned"
+        lib = spmv_hw.load(np.float32)
+        n, z = 10_000_000, 160_000_000
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+        x = spmv_hw.gen_vector(lib, n, seed=6)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+        y = torch.empty(n, dtype=torch.float32, device="cuda")
+        for _ in range(5):
+            plan.run(x, y)
+        torch.cuda.synchronize()
+        st = plan.stats()
+        out = {"matrix": "powerlaw 10M/160M fp32", "kernel": st["kernel"]}
+        for k in (0, 1):  # every slot, trimmed to the workgroups that ran (unused slots stay 0)
+            raw = read_stamps(lib, 4096, k)
+            out["pass%d" % (k + 1)] = bin_pass(raw[raw[:, 1] > 0])
+        print(json.dumps(out), flush=True)
+        return
     lib = spmv_hw.load(np.float64)
     n, z = 10_000_000, 160_000_000
     rp_full, _ = lib.powerlaw_row_ptr(n, z, n, 4)
