@@ -70,8 +70,21 @@ constexpr int kBinU = 4;     // pass 1: 64-lane steps of loads in flight per wav
 constexpr int kBinD = 8;     // pass 2: steps in flight per wave
 constexpr int kBinStageLoads = 10;  // pass 1: 16-B x loads per thread staging a window
 constexpr uint64_t kBinAlign = 128;  // entries: window ranges and pass-1 units start at multiples
+constexpr double kBinXccBias = 0.0;  // pass-1 window bias by default on a 256-CU chip (build_binned)
 constexpr uint16_t kBinSent = 0xFFFF;  // column offset of a pad entry: its product is exactly +0
                                        // (W <= 40960, so no real offset takes this value)
+
+// Window geometry: even windows W0 columns wide, odd ones W1 (W0 = W1 = W unless the pass-1 XCC
+// bias is on, build_binned); window pair k spans columns [k (W0 + W1), (k + 1) (W0 + W1)).
+__host__ __device__ __forceinline__ uint32_t bin_win_of(uint32_t c, uint32_t W0, uint32_t W1)
+{
+    const uint32_t pw = W0 + W1, k = c / pw;
+    return 2 * k + (c - k * pw >= W0 ? 1u : 0u);
+}
+__host__ __device__ __forceinline__ uint64_t bin_win_base(uint32_t w, uint32_t W0, uint32_t W1)
+{
+    return uint64_t(w >> 1) * (W0 + W1) + (w & 1u) * W0;
+}
 
 // delta bytes of one lane's PER entries (delta layout)
 template <int PER> struct BinDelta;
@@ -104,7 +117,7 @@ __device__ unsigned long long g_abl_bin[2][4 * 4096];
 // POL (variants 3-5, the same y): bit 0 = temporal (default-policy) product stores instead of
 // non-temporal ones, bit 1 = temporal entry loads
 template <typename V, bool AL, int POL = 0>
-__global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint32_t ncols, uint32_t W,
+__global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint32_t ncols, uint32_t W0, uint32_t W1,
                                                    const uint64_t *__restrict__ ub, const uint32_t *__restrict__ uwin,
                                                    const uint16_t *__restrict__ colw, const V *__restrict__ val,
                                                    V *__restrict__ prod)
@@ -116,8 +129,8 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
     constexpr int PER = 16 / sizeof(V);
     BN_STAMP(0, 0);
     const uint32_t u = blockIdx.x;
-    const uint64_t c0 = (uint64_t)uwin[u] * W;
-    const uint32_t wn = (uint32_t)std::min<uint64_t>(W, ncols - c0);  // columns of this window
+    const uint64_t c0 = bin_win_base(uwin[u], W0, W1);
+    const uint32_t wn = (uint32_t)std::min<uint64_t>(uwin[u] & 1 ? W1 : W0, ncols - c0);  // columns of this window
     if (AL) {
         VT t[kBinStageLoads];
 #pragma unroll
@@ -354,8 +367,8 @@ __device__ __forceinline__ uint32_t bin_row_of(const IndexType *__restrict__ rp,
 
 // per entry: segment key (window * npan + panel), row offset in its panel; segment counts
 __global__ void k_bin_keys(const IndexType *__restrict__ rp, IndexType n, const IndexType *__restrict__ col,
-                           uint64_t nnz, const uint32_t *__restrict__ panel_row, uint32_t npan, uint32_t W,
-                           uint32_t *__restrict__ key, uint16_t *__restrict__ rowp, uint32_t *__restrict__ cnt)
+                           uint64_t nnz, const uint32_t *__restrict__ panel_row, uint32_t npan, uint32_t W0,
+                           uint32_t W1, uint32_t *__restrict__ key, uint16_t *__restrict__ rowp, uint32_t *__restrict__ cnt)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nnz)
@@ -369,7 +382,7 @@ __global__ void k_bin_keys(const IndexType *__restrict__ rp, IndexType n, const 
         else
             hi = mid;
     }
-    const uint32_t k = (col[j] / W) * npan + lo;
+    const uint32_t k = bin_win_of(col[j], W0, W1) * npan + lo;
     key[j] = k;
     rowp[j] = (uint16_t)(r - panel_row[lo]);
     atomicAdd(&cnt[k], 1u);
@@ -378,7 +391,7 @@ __global__ void k_bin_keys(const IndexType *__restrict__ rp, IndexType n, const 
 template <typename V>
 __global__ void k_bin_scatter(const uint32_t *__restrict__ key, const uint16_t *__restrict__ rowp_in,
                               const IndexType *__restrict__ col, const V *__restrict__ val_in, uint64_t nnz,
-                              uint32_t npan, uint32_t W, const uint64_t *__restrict__ seg,
+                              uint32_t npan, uint32_t W0, uint32_t W1, const uint64_t *__restrict__ seg,
                               uint32_t *__restrict__ cursor, V *__restrict__ val, uint16_t *__restrict__ colw,
                               uint16_t *__restrict__ rowp)
 {
@@ -388,7 +401,7 @@ __global__ void k_bin_scatter(const uint32_t *__restrict__ key, const uint16_t *
     const uint32_t k = key[j];
     const uint64_t d = seg[k] + atomicAdd(&cursor[k], 1u);
     val[d] = val_in[j];
-    colw[d] = (uint16_t)(col[j] - (k / npan) * W);
+    colw[d] = (uint16_t)(col[j] - bin_win_base(k / npan, W0, W1));
     rowp[d] = rowp_in[j];
 }
 
@@ -427,7 +440,8 @@ __global__ void k_bin_gaps(const uint64_t *__restrict__ k64, uint64_t nnz, uint3
 template <typename V>
 __global__ void k_bin_scatter_delta(const uint64_t *__restrict__ k64, const uint32_t *__restrict__ idx,
                                     const uint32_t *__restrict__ pscan, const uint64_t *__restrict__ sorted_off,
-                                    uint64_t nnz, uint32_t npan, uint32_t W, const IndexType *__restrict__ col,
+                                    uint64_t nnz, uint32_t npan, uint32_t W0, uint32_t W1,
+                                    const IndexType *__restrict__ col,
                                     const V *__restrict__ val_in, const uint64_t *__restrict__ seg,
                                     V *__restrict__ val, uint16_t *__restrict__ colw, uint8_t *__restrict__ delta)
 {
@@ -448,7 +462,7 @@ __global__ void k_bin_scatter_delta(const uint64_t *__restrict__ k64, const uint
     }
     const uint32_t j = idx[k];
     val[d] = val_in[j];
-    colw[d] = (uint16_t)(col[j] - (uint32_t)(sg / npan) * W);
+    colw[d] = (uint16_t)(col[j] - bin_win_base((uint32_t)(sg / npan), W0, W1));
     delta[d] = (uint8_t)(gap - 255u * e);
 }
 
@@ -480,7 +494,7 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
     if (p.nr_rows == 0)
         return hipSuccess;
     if (p.b_nunits) {
-        const size_t lds1 = size_t(p.b_W) * sizeof(ValueType);
+        const size_t lds1 = size_t(std::max(p.b_W, p.b_W1)) * sizeof(ValueType);
         const bool al = (reinterpret_cast<uintptr_t>(d_x) & 15u) == 0;
         // pass-1 cache policy: temporal product stores when the products fit well within
         // reach of the 256 MB MALL (fp32 10M/160M: 640 MB, 0.460 vs 0.487 ms; fp64 1.28 GB:
@@ -492,15 +506,15 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
         if (pol && al) {
 #define BINPOL(P)                                                                                          \
     launch_or_warm(warm, k_bin_mul<ValueType, true, P>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x, \
-                   (uint32_t)p.nr_cols, p.b_W, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod)
+                   (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod)
             if (pol == 1) BINPOL(1); else if (pol == 2) BINPOL(2); else BINPOL(3);
 #undef BINPOL
         } else if (al || warm)
             launch_or_warm(warm, k_bin_mul<ValueType, true>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x,
-                           (uint32_t)p.nr_cols, p.b_W, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
+                           (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
         if (!al || warm)
             launch_or_warm(warm, k_bin_mul<ValueType, false>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x,
-                           (uint32_t)p.nr_cols, p.b_W, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
+                           (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
     }
     const size_t lds2 = (size_t(p.panel_rmax) + 1) * sizeof(double);
     // variants 1 / 2 (tests): segment offsets rebased past 2^31 / 2^32, the product and row arrays
@@ -556,6 +570,29 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         nwin = std::min<uint64_t>(cus * rounds, (ncols + PER - 1) / PER);
         W = ((ncols + nwin - 1) / nwin + PER - 1) / PER * PER;
         nwin = (ncols + W - 1) / W;
+    }
+    // Pass-1 XCC bias: unit u runs on XCC u % 8 (tools/xcc_map_probe.py), and on the boxes
+    // measured pass 1's one-window workgroups take 266 us on even XCCs against 280 us on odd ones
+    // (tools/wg_timeline.py --binned, profiles/r03bn_binned_timeline.jsonl). With one unit per
+    // window (nwin a whole number of rounds) even windows get W (1 + d) columns, odd ones
+    // W (1 - d): every pair still spans 2W, so a column's window stays closed-form
+    // (bin_win_of). Env SPMV_BIN_XCC_BIAS=d (0 = even widths); only on a whole 256-CU chip.
+    uint64_t W0 = W, W1 = W;
+    {
+        const char *xb = std::getenv("SPMV_BIN_XCC_BIAS");
+        double d = xb ? std::atof(xb) : (cus == 256 ? kBinXccBias : 0.0);
+        if (!(d > -0.25 && d < 0.25) || nwin < (uint64_t)cus || nwin % cus)
+            d = 0.0;
+        const uint64_t w0 = std::min<uint64_t>(wmax, (uint64_t(std::llround(W * (1.0 + d))) + PER / 2) / PER * PER);
+        if (d != 0.0 && w0 >= PER && w0 < 2 * W) {
+            W0 = w0;
+            W1 = 2 * W - w0;
+            if (W1 > wmax) {  // a negative bias past the LDS: even widths
+                W0 = W1 = W;
+            }
+            const uint64_t pw = W0 + W1, k = ncols / pw, rem = ncols - k * pw;
+            nwin = 2 * k + (rem == 0 ? 0 : rem <= W0 ? 1 : 2);
+        }
     }
     // panels: y of <= rmax rows in LDS (fp64), plus the scratch slot of the pad entries
     const uint32_t rmax = (uint32_t)std::min<uint64_t>((kSweepLdsBytes - 256) / 8 - 1, 65534);
@@ -617,7 +654,8 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     p.npanels = P;
     p.panel_rmax = rmax_used;
     p.b_nwin = (uint32_t)nwin;
-    p.b_W = (uint32_t)W;
+    p.b_W = (uint32_t)W0;
+    p.b_W1 = (uint32_t)W1;
     SPMV_TRY(hipMalloc((void **)&p.d_panel_row, (P + 1) * 4));
     SPMV_TRY(hipMemcpyAsync(p.d_panel_row, prow.data(), (P + 1) * 4, hipMemcpyHostToDevice, s));
 
@@ -662,7 +700,7 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         BN_TRY(hipMalloc((void **)&d_key, nnz * 4));
         BN_TRY(hipMalloc((void **)&d_rowp_tmp, nnz * 2));
         hipLaunchKernelGGL(k_bin_keys, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_rp, n, d_col_src, nnz,
-                           p.d_panel_row, P, (uint32_t)W, d_key, d_rowp_tmp, d_cnt);
+                           p.d_panel_row, P, (uint32_t)W0, (uint32_t)W1, d_key, d_rowp_tmp, d_cnt);
         BN_TRY(hipGetLastError());
         BN_TRY(hipMemcpyAsync(cnt.data(), d_cnt, nseg * 4, hipMemcpyDeviceToHost, s));
         BN_TRY(hipStreamSynchronize(s));
@@ -775,7 +813,7 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     BN_TRY(hipMalloc((void **)&p.d_b_rowp, alloc * (delta ? 1 : 2)));
     if (nnz && delta) {
         hipLaunchKernelGGL((k_bin_scatter_delta<ValueType>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s,
-                           d_k64s, d_idxs, d_pscan, d_soff, nnz, P, (uint32_t)W, d_col_src, d_val_src, p.d_b_seg,
+                           d_k64s, d_idxs, d_pscan, d_soff, nnz, P, (uint32_t)W0, (uint32_t)W1, d_col_src, d_val_src, p.d_b_seg,
                            p.d_b_val, p.d_b_colw, reinterpret_cast<uint8_t *>(p.d_b_rowp));
         BN_TRY(hipGetLastError());
         BN_TRY(hipMemcpyAsync(d_esc, esc.data(), nseg * 4, hipMemcpyHostToDevice, s));
@@ -786,7 +824,7 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         BN_TRY(hipMalloc((void **)&d_cur, nseg * 4));
         BN_TRY(hipMemsetAsync(d_cur, 0, nseg * 4, s));
         hipLaunchKernelGGL((k_bin_scatter<ValueType>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_key,
-                           d_rowp_tmp, d_col_src, d_val_src, nnz, P, (uint32_t)W, p.d_b_seg, d_cur, p.d_b_val,
+                           d_rowp_tmp, d_col_src, d_val_src, nnz, P, (uint32_t)W0, (uint32_t)W1, p.d_b_seg, d_cur, p.d_b_val,
                            p.d_b_colw, reinterpret_cast<uint16_t *>(p.d_b_rowp));
         BN_TRY(hipGetLastError());
         hipLaunchKernelGGL((k_bin_pad<ValueType, false>), dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, nseg,

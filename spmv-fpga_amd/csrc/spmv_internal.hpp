@@ -164,6 +164,7 @@ struct spmv_plan {
     // binned representation (kernel 6, binned.hip): reuses npanels, panel_rmax, d_panel_row and
     // ent_pad of the sweep fields; entries ordered (window, panel), segments padded
     uint32_t b_nwin = 0, b_W = 0;      // column windows of b_W columns (x staged in LDS by pass 1)
+    uint32_t b_W1 = 0;                 // width of the odd windows (b_W: the even ones; XCC bias)
     uint64_t b_nunits = 0;             // pass-1 work units
     ValueType *d_b_val = nullptr;
     uint16_t *d_b_colw = nullptr;      // column - window base

@@ -1279,3 +1279,31 @@ def test_sweep_xcc_bias(torch, monkeypatch, shape, bias):
     assert not np.isnan(yy).any()
     ref = oracle.spmv_gold(row_ptr, c, v, xx)
     assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(np.float64)]
+
+
+@pytest.mark.parametrize("bias", ["0.025", "0.2", "-0.1", "0"])
+@pytest.mark.parametrize("dtype,m", [(np.float32, 300_001), (np.float64, 6_000_001)])
+@pytest.mark.parametrize("aligned", [True, False])
+def test_binned_xcc_bias_windows(torch, monkeypatch, bias, dtype, m, aligned):
+    """Pass-1 XCC bias (SPMV_BIN_XCC_BIAS=d, binned.hip build_binned): even windows W (1 + d)
+    columns wide, odd ones W (1 - d), so a column's window and offset come from the closed form
+    bin_win_of / bin_win_base in the key build, the scatter and k_bin_mul. Columns cover every
+    window (one round of 256 windows in fp32, two rounds in fp64 where W is LDS-capped), a
+    partial last pair, a negative and a large bias; x aligned and one element in."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "binned")
+    monkeypatch.setenv("SPMV_BIN_XCC_BIAS", bias)
+    rng = np.random.default_rng(31)
+    n = 3000
+    row_ptr, col, val, x = random_csr(rng, n, m, rng.integers(0, 30, n), dtype)
+    col[-1] = m - 1  # the last column of the last (partial) window
+    col[0] = 0
+    lib = spmv_hw.load(dtype)
+    plan = spmv_hw.Plan.from_device(lib, to_dev(torch, row_ptr), to_dev(torch, col), to_dev(torch, val), m)
+    assert plan.stats()["kernel"] == KERNEL_ID["binned"]
+    off = 0 if aligned else 1
+    xb = to_dev(torch, np.concatenate([np.zeros(off, dtype), x]))
+    y = torch.full((n,), float("nan"), dtype=xb.dtype, device="cuda")
+    plan.run(xb[off:], y)
+    torch.cuda.synchronize()
+    plan.destroy()
+    check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y.cpu().numpy(), dtype)

@@ -83,8 +83,8 @@ def main():
             if k not in plans:  # "sweep@512" = 512-thread workgroups, "sweepU" = unpacked entries
                 kern, _, threads = k.partition("@")
                 kern, _, xbias = kern.partition("~")  # "sweep~0.012": SPMV_SWEEP_XCC_BIAS=0.012
-                if xbias:
-                    os.environ["SPMV_SWEEP_XCC_BIAS"] = xbias
+                if xbias:  # "binned~0.025": SPMV_BIN_XCC_BIAS (pass-1 window widths)
+                    os.environ["SPMV_BIN_XCC_BIAS" if kern.startswith("binned") else "SPMV_SWEEP_XCC_BIAS"] = xbias
                 if kern.endswith("U"):
                     kern = kern[:-1]
                     os.environ["SPMV_SWEEP_PACKED"] = "0"
@@ -133,6 +133,7 @@ def main():
                 os.environ.pop("SPMV_SLICE_ACC", None)
                 os.environ.pop("SPMV_SWEEP_DETERMINISTIC", None)
                 os.environ.pop("SPMV_SWEEP_XCC_BIAS", None)
+                os.environ.pop("SPMV_BIN_XCC_BIAS", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
