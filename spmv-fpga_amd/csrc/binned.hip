@@ -808,7 +808,14 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         BN_TRY(hipMemcpyAsync(p.d_b_uwin, uwin.data(), uwin.size() * 4, hipMemcpyHostToDevice, s));
     const uint64_t alloc = std::max<uint64_t>(ent_pad, PER);
     BN_TRY(hipMalloc((void **)&p.d_b_val, alloc * sizeof(ValueType)));
-    BN_TRY(hipMalloc((void **)&p.d_b_prod, alloc * sizeof(ValueType)));
+    {
+        // env SPMV_BIN_PROD_SKEW=bytes (measurement): the products start that far (a multiple of
+        // 256 B) into their allocation, shifting their address bits against the entry arrays'
+        const char *sk = std::getenv("SPMV_BIN_PROD_SKEW");
+        const uint64_t skew = sk ? (uint64_t)std::strtoull(sk, nullptr, 10) / 256 * 256 : 0;
+        BN_TRY(hipMalloc(&p.d_b_prod_alloc, alloc * sizeof(ValueType) + skew));
+        p.d_b_prod = reinterpret_cast<ValueType *>(static_cast<unsigned char *>(p.d_b_prod_alloc) + skew);
+    }
     BN_TRY(hipMalloc((void **)&p.d_b_colw, alloc * 2));
     BN_TRY(hipMalloc((void **)&p.d_b_rowp, alloc * (delta ? 1 : 2)));
     if (nnz && delta) {

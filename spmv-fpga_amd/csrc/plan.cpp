@@ -654,7 +654,7 @@ spmv_plan::~spmv_plan()
                       (void *)d_s_cbase, (void *)d_s_row16, (void *)d_s_d8, (void *)d_s_dbase, (void *)d_s_side, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
                       (void *)d_sbase, (void *)d_slice_len, (void *)d_b_val, (void *)d_b_colw, (void *)d_b_rowp,
-                      (void *)d_b_prod, (void *)d_b_seg, (void *)d_b_seg_hi, (void *)d_b_ub, (void *)d_b_uwin})
+                      d_b_prod_alloc, (void *)d_b_seg, (void *)d_b_seg_hi, (void *)d_b_ub, (void *)d_b_uwin})
         if (ptr)
             (void)hipFree(ptr);
     for (hipEvent_t e : ev)

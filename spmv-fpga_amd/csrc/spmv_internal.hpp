@@ -173,6 +173,7 @@ struct spmv_plan {
     bool b_prod_temporal = false;      // pass 1 stores the products with the default cache policy
                                        // (they stay partly in MALL for pass 2): products <= 1 GiB
     ValueType *d_b_prod = nullptr;     // products, written by pass 1 and read by pass 2
+    void *d_b_prod_alloc = nullptr;    // its allocation (d_b_prod may start past its base)
     uint64_t *d_b_seg = nullptr;       // padded segment offsets [b_nwin * npanels + 1]
     uint64_t *d_b_seg_hi = nullptr;    // variants 1 / 2 (tests): d_b_seg + b_seg_base, read by pass 2
     uint64_t b_seg_base = 0;           // with prod / rowp rebased by -b_seg_base (same addresses)

@@ -82,6 +82,9 @@ def main():
             k, var = v.split(":")
             if k not in plans:  # "sweep@512" = 512-thread workgroups, "sweepU" = unpacked entries
                 kern, _, threads = k.partition("@")
+                kern, _, pskew = kern.partition("^")  # "binned^4096": SPMV_BIN_PROD_SKEW=4096
+                if pskew:
+                    os.environ["SPMV_BIN_PROD_SKEW"] = pskew
                 kern, _, xbias = kern.partition("~")  # "sweep~0.012": SPMV_SWEEP_XCC_BIAS=0.012
                 if xbias:  # "binned~0.025": SPMV_BIN_XCC_BIAS (pass-1 window widths)
                     os.environ["SPMV_BIN_XCC_BIAS" if kern.startswith("binned") else "SPMV_SWEEP_XCC_BIAS"] = xbias
@@ -134,6 +137,7 @@ def main():
                 os.environ.pop("SPMV_SWEEP_DETERMINISTIC", None)
                 os.environ.pop("SPMV_SWEEP_XCC_BIAS", None)
                 os.environ.pop("SPMV_BIN_XCC_BIAS", None)
+                os.environ.pop("SPMV_BIN_PROD_SKEW", None)
         os.environ.pop("SPMV_HW_KERNEL", None)
         st = next(iter(plans.values())).stats()
         del rp, col, val
