@@ -839,8 +839,8 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         BN_TRY(hipGetLastError());
     }
     BN_TRY(hipStreamSynchronize(s));
-#undef BN_TRY
     cleanup();
+#undef BN_TRY
     return 0;
 }
 
