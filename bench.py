@@ -43,6 +43,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -52,16 +55,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spmv-fpga_amd"))
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-import spmv_dist  # noqa: E402
-import spmv_hw  # noqa: E402
-
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -96,10 +93,94 @@ def parse():
                     help="threads of the row-parallel CPU line (the box's CPU share is 16)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
-    a = ap.parse_args()
+    ap.add_argument("--spawn-grace", type=float, default=60.0,
+                    help="self-launch: seconds the other ranks may run on after one rank failed")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="every rank prints its launch environment as JSON and exits before any GPU call")
+    ap.add_argument("--dry-launch-rc", default="",
+                    help="with --dry-launch: RANK:RC[,RANK:RC] exit codes of those ranks (launcher tests; "
+                         "RC < 0 kills the rank with signal -RC, 'hang' makes it sleep)")
+    a = ap.parse_args(argv)
     if a.scaling is None:
         a.scaling = "strong" if a.gpus > 1 else "weak"
     return a
+
+
+# ---- self-launch: `bench.py --gpus N` with no torchrun around it ---------------------------------
+# The driver may start the N-GPU bench as `python bench.py --gpus N` (no launcher). Then this
+# process starts N workers itself -- one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+# MASTER_ADDR / MASTER_PORT set as torch.distributed.run would -- before torch is even imported here
+# (no HIP call happens in the parent), relays rank 0's JSON line (rank 0 writes to this stdout,
+# the other ranks to stderr) and exits with the workers' worst status.
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _status(rc):
+    """A worker's exit status as a shell would report it (a signal k -> 128 + k)."""
+    return 128 - rc if rc is not None and rc < 0 else (rc or 0)
+
+
+def spawn_ranks(args, argv):
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPMV_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+
+    def stop(signum, _frame):  # the parent is being stopped: take the workers with it
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        sys.exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, stop)
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > args.spawn_grace:
+            for p in procs:  # a rank died: the others may wait in a collective forever
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    return max(_status(p.returncode) for p in procs)
+
+
+def dry_launch(args):
+    """--dry-launch: this rank's launch environment, before any GPU call; rank 0 on stdout."""
+    env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                                          "MASTER_ADDR", "MASTER_PORT", "SPMV_BENCH_LAUNCHER")}
+    rank = int(os.environ.get("RANK", "0"))
+    print(json.dumps({"dry_launch": True, "gpus": args.gpus, "pid": os.getpid(), **env}), flush=True)
+    codes = dict(kv.split(":") for kv in args.dry_launch_rc.split(",") if kv)
+    code = codes.get(str(rank), "0")
+    if code == "hang":
+        time.sleep(3600)
+    if int(code) < 0:
+        os.kill(os.getpid(), -int(code))
+    return int(code)
+
+
+if __name__ == "__main__":
+    _args = parse()
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(_args, sys.argv[1:]))
+    if _args.dry_launch:
+        sys.exit(dry_launch(_args))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import spmv_dist  # noqa: E402
+import spmv_hw  # noqa: E402
 
 
 def setup_dist(args):
@@ -108,7 +189,7 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
+    if world != args.gpus:  # (without WORLD_SIZE, --gpus N > 1 self-launches N ranks: spawn_ranks)
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     backend = os.environ.get("SPMV_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
@@ -464,7 +545,8 @@ def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
         if mg is not None:
             mg.destroy()
         return {"error": err or "spmv_mgpu_create_rank failed on another rank"}
-    res = {"api": "spmv_mgpu_create_rank + spmv_mgpu_run (library RCCL clique, one rank per GPU)"}
+    res = {"api": "spmv_mgpu_create_rank + spmv_mgpu_run (library RCCL clique, one rank per GPU)",
+           "rccl_comm_count": mg.comm_count()}
     mg.set_x_device(x)
     for name, mode in (("gather", spmv_hw.MGPU_GATHER), ("reduce", spmv_hw.MGPU_REDUCE),
                        ("allgather", spmv_hw.MGPU_ALLGATHER)):
@@ -584,6 +666,54 @@ def strong_companion(lib, args, world, rank, dev, stream):
     res["e2e_gflops_with_reduce"] = round(2.0 * nnz_all / ((ms + res["reduce_ms"]) * 1e-3) / 1e9, 2)
     res["e2e_gflops_with_gather"] = round(2.0 * nnz_all / ((ms + res["gather_ms"]) * 1e-3) / 1e9, 2)
     plan.destroy()
+    return res
+
+
+def distributed_parity(lib, args, world, rank, dev, y, st):
+    """N > 1: the reference checks every spmv_hw result (main.cpp:77-82); so does this line.
+    Strong scaling (config 4): every rank's y slice is gathered on rank 0 (spmv_dist.exchange_gather)
+    and the assembled 10M-row y is checked against the oracle's spmv_gold of the whole matrix,
+    regenerated on rank 0 by the same generator. Weak scaling (and the banded workload): every
+    rank checks its own partition; the worst error over ranks is reported. Runs after the timed
+    region, never inside it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    dtype = np.float64 if args.dtype == "f64" else np.float32
+    tol = 1e-6 if dtype == np.float64 else 1e-4
+
+    def check(rp, col, val, x, y_test):
+        h = [t.cpu().numpy() for t in (rp, col, val, x)]
+        r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+        ref = oracle.spmv_gold(r, c, h[2], h[3])
+        yt = y_test.cpu().numpy() if hasattr(y_test, "cpu") else y_test
+        return oracle.scaled_error(r, c, h[2], h[3], ref, yt), oracle.verification_errors(ref, yt.astype(ref.dtype))
+
+    if args.scaling == "strong" and args.workload == "powerlaw":
+        cnt = [0.0] * world
+        cnt[rank] = float(st["nr_rows"])
+        counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
+        y_full = spmv_dist.exchange_gather(y, counts)
+        res = {"scope": f"y of all {world} row slices gathered on rank 0 vs spmv_gold of the whole matrix",
+               "rows_checked": int(counts.sum())}
+        if rank == 0:
+            n, z = args.rows or 10_000_000, args.nnz or 160_000_000
+            rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+            x = spmv_hw.gen_vector(lib, n, seed=6)
+            err, nerr = check(rp, col, val, x, y_full)
+            del rp, col, val, x
+            torch.cuda.empty_cache()
+        else:
+            err, nerr = 0.0, 0
+    else:
+        rp, col, val, x, _, _ = build_workload(lib, args, world, rank)
+        err, nerr = check(rp, col, val, x, y)
+        del rp, col, val, x
+        torch.cuda.empty_cache()
+        res = {"scope": f"every rank's own partition vs spmv_gold (worst of {world} ranks)",
+               "rows_checked": int(spmv_dist.sum_over_ranks([float(st["nr_rows"])], dev)[0])}
+    err = spmv_dist.max_over_ranks(err, dev)
+    nerr = int(spmv_dist.sum_over_ranks([float(nerr)], dev)[0])
+    res.update({"max_scaled_err": err, "tol": tol, "ref_abs_1e-5_errors": nerr, "pass": bool(err <= tol)})
     return res
 
 
@@ -755,6 +885,8 @@ def main():
         "value": round(gflops, 3),
         "unit": "GFLOP/s",
         "n_gpus": world,
+        "n_ranks": dist.get_world_size() if dist.is_initialized() else 1,
+        "launcher": os.environ.get("SPMV_BENCH_LAUNCHER") or ("torch.distributed.run" if world > 1 else None),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 5),
@@ -895,7 +1027,8 @@ def main():
                 res["native"] = {"error": str(e)[:300]}
         return res
 
-    if world > 1:
+    if world > 1:  # correctness first: the parity of this very run, then the side measurements
+        guarded("parity", lambda: distributed_parity(lib, args, world, rank, dev, y, st))
         guarded("exchange", exchange_fields)
     if world > 1 and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
         guarded("strong_companion", lambda: strong_companion(lib, args, world, rank, dev, stream))

@@ -213,6 +213,36 @@ int spmv_mgpu_set_x_device_on(spmv_mgpu *mg, const ValueType *d_x, void *stream)
 /* device address of this process's y (rank 0's y for a gather / reduce; the local x = y after
  * an all-gather), for callers that keep y on the GPU */
 int spmv_mgpu_y_device(spmv_mgpu *mg, int exchange, ValueType **d_y);
+/* Ranks in the handle's RCCL communicator (ncclCommCount of its first local device). */
+int spmv_mgpu_comm_count(const spmv_mgpu *mg, int *count);
+
+/* The schedule of one SpMV step of rank `rank` (of `nranks`, slices bounds[0..nranks]): the ops
+ * that spmv_mgpu_run, _run_pipelined and _run_graph issue for that rank, in order. It is the
+ * reference's merge loop (accum_results, csr_hw.cpp:1531-1565, over the CUs of
+ * csr_hw_wrapper.cpp:276-281) as data: every RCCL call of the exchange iterates over this list,
+ * and tests/test_exchange_schedule.py replays the same lists over torch.distributed (gloo) on the
+ * CPU. Local ops (ZERO, COMPUTE) come first and run on the compute stream; the exchange ops
+ * (SEND and up) follow inside one RCCL group. Host only, no GPU needed. Returns the number of
+ * ops (only the first `cap` are written; ops may be NULL to count), or -1 on bad arguments. */
+typedef struct spmv_xop {
+    int32_t kind;    /* SPMV_XOP_* */
+    int32_t buf;     /* SPMV_XBUF_*: the rank's buffer the op writes or sends */
+    int32_t peer;    /* SEND: destination rank, RECV: source rank, REDUCE / BCAST: root; else -1 */
+    int32_t out;     /* REDUCE: SPMV_XBUF_Y on the root (the sum lands there), else -1 */
+    uint32_t offset; /* first element of the op within buf */
+    uint32_t count;  /* elements */
+} spmv_xop;
+#define SPMV_XOP_ZERO 0    /* buf[offset, offset + count) = 0 */
+#define SPMV_XOP_COMPUTE 1 /* buf[offset, offset + count) = rows [bounds[rank], bounds[rank + 1]) of A x */
+#define SPMV_XOP_SEND 2    /* ncclSend(buf + offset, count, peer) */
+#define SPMV_XOP_RECV 3    /* ncclRecv(buf + offset, count, peer) */
+#define SPMV_XOP_REDUCE 4  /* ncclReduce(buf + offset -> out + offset, count, sum, root = peer) */
+#define SPMV_XOP_BCAST 5   /* ncclBroadcast(buf + offset, in place, count, root = peer) */
+#define SPMV_XBUF_Y 0      /* rank 0's full y (nr_rows) */
+#define SPMV_XBUF_SLICE 1  /* rank > 0, gather: its own rows (bounds[rank + 1] - bounds[rank]) */
+#define SPMV_XBUF_PART 2   /* reduce: the full-length partial (zero outside the rank's rows) */
+#define SPMV_XBUF_XNEXT 3  /* all-gather: the full-length next x of every rank */
+int spmv_mgpu_schedule(int exchange, int rank, int nranks, const IndexType *bounds, spmv_xop *ops, int cap);
 
 /* ---------------- synthetic inputs (bench/test infrastructure) ---------------- */
 /* Banded: n x n, `width` non-zeros per row, columns [clamp(i - width/2, 0, n - width), +width),

@@ -579,7 +579,7 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     // (bin_win_of). Env SPMV_BIN_XCC_BIAS=d (0 = even widths); only on a whole 256-CU chip.
     uint64_t W0 = W, W1 = W;
     {
-        const char *xb = std::getenv("SPMV_BIN_XCC_BIAS");
+        const char *xb = ablation_env("SPMV_BIN_XCC_BIAS");
         double d = xb ? std::atof(xb) : (cus == 256 ? kBinXccBias : 0.0);
         if (!(d > -0.25 && d < 0.25) || nwin < (uint64_t)cus || nwin % cus)
             d = 0.0;
@@ -712,7 +712,7 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     std::vector<uint32_t> esc(nseg, 0);
     bool delta = false;
     {
-        const char *denv = std::getenv("SPMV_BIN_DELTA");
+        const char *denv = ablation_env("SPMV_BIN_DELTA");
         const bool never = denv && denv[0] == '0', always = denv && denv[0] == '1';
         delta = !nnz && always;  // an empty slice: either form reads nothing
         if (nnz && !never) {
@@ -811,7 +811,7 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     {
         // env SPMV_BIN_PROD_SKEW=bytes (measurement): the products start that far (a multiple of
         // 256 B) into their allocation, shifting their address bits against the entry arrays'
-        const char *sk = std::getenv("SPMV_BIN_PROD_SKEW");
+        const char *sk = ablation_env("SPMV_BIN_PROD_SKEW");
         const uint64_t skew = sk ? (uint64_t)std::strtoull(sk, nullptr, 10) / 256 * 256 : 0;
         BN_TRY(hipMalloc(&p.d_b_prod_alloc, alloc * sizeof(ValueType) + skew));
         p.d_b_prod = reinterpret_cast<ValueType *>(static_cast<unsigned char *>(p.d_b_prod_alloc) + skew);

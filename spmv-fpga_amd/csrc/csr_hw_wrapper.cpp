@@ -4,10 +4,10 @@
 // csr_hw.cpp:459). x is replicated on every GPU in use (the reference copies x into every CU's
 // BRAM, spmv.cpp:280-294). spmv_hw runs every unit's kernels, then adds each unit's y slice
 // into the caller's y_fpga (the role of accum_results, csr_hw.cpp:1531-1565, and the loop
-// csr_hw_wrapper.cpp:276-281), printing the reference's timing lines. When the units sit on
-// distinct GPUs the slices first meet on GPU 0 over xGMI (an RCCL gather of the disjoint slices,
-// or with SPMV_HW_MERGE=reduce the literal ncclReduce(sum) of full-length partials), and one
-// D2H copy brings y to the host; SPMV_HW_MERGE=host keeps the per-GPU PCIe merge.
+// csr_hw_wrapper.cpp:276-281), printing the reference's timing lines. By default every GPU's
+// slice comes back over its own PCIe link (SPMV_HW_MERGE=auto|host); with SPMV_HW_MERGE=gather
+// (or reduce) the slices first meet on GPU 0 over xGMI (an RCCL gather of the disjoint slices,
+// or the literal ncclReduce(sum) of full-length partials) and one D2H copy brings y to the host.
 #include <sys/mman.h>
 #include <sys/time.h>
 
@@ -40,14 +40,6 @@ void check(hipError_t e, const char *what)
         die(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// util.cpp:3-8 — wall clock in microseconds
-double timestamp_us()
-{
-    struct timeval tv;
-    gettimeofday(&tv, nullptr);
-    return tv.tv_usec + tv.tv_sec * 1e6;
-}
-
 int device_count()
 {
     int n = 0;
@@ -71,7 +63,7 @@ struct d2h_events {
         while (ev.size() <= k) {
             hipEvent_t e = nullptr;
             check(hipSetDevice(device), "hipSetDevice");
-            const char *bs = std::getenv("SPMV_HW_BLOCKING_SYNC");
+            const char *bs = ablation_env("SPMV_HW_BLOCKING_SYNC");
             check(hipEventCreateWithFlags(&e, hipEventDisableTiming | (bs && bs[0] == '1' ? hipEventBlockingSync : 0)),
                   "hipEventCreate");
             ev.push_back(e);
@@ -165,34 +157,16 @@ void alloc_y_scratch(hw_matrix_impl *m)
           "hipHostMalloc(y stage)");
 }
 
-// Maps the caller's y pages writable while the DMA runs, keeping their contents: a fresh
-// calloc'd y_fpga (main.cpp:74) otherwise takes one page fault per 4 KiB inside the adds
-void prefault(ValueType *p, uint64_t count)
-{
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23  // Linux 5.14
-#endif
-    const uintptr_t pg = 4096;
-    const uintptr_t b = ((uintptr_t)p + pg - 1) & ~(pg - 1), e = (uintptr_t)(p + count) & ~(pg - 1);
-    if (e <= b || madvise((void *)b, e - b, MADV_POPULATE_WRITE) == 0)
-        return;
-    for (uintptr_t a = b; a < e; a += pg) {  // older kernels: touch each page
-        volatile ValueType *q = (volatile ValueType *)a;
-        *q = *q;
-    }
-}
-
 uint64_t ceil16(uint64_t bytes) { return (bytes + 15) / 16; }
 
-// auto (default): the RCCL gather when there are >= 2 units and each has a GPU of its own, else
-// the host merge; host | gather | reduce force one (gather / reduce need one unit per GPU)
+// auto (default) and host: the host merge (y_fpga is host memory: G slices come back over G PCIe
+// links at once); gather | reduce: the RCCL forms (one unit per GPU; they fail
+// fast when RCCL cannot form the clique)
 int merge_mode(int units)
 {
     const char *e = std::getenv("SPMV_HW_MERGE");
     const int ndev = device_count();
-    if (!e || !*e || !std::strcmp(e, "auto"))
-        return units >= 2 && units <= ndev ? kMergeGather : kMergeHost;
-    if (!std::strcmp(e, "host"))
+    if (!e || !*e || !std::strcmp(e, "auto") || !std::strcmp(e, "host"))
         return kMergeHost;
     const int m = !std::strcmp(e, "gather") ? kMergeGather : !std::strcmp(e, "reduce") ? kMergeReduce : -1;
     if (m < 0)
@@ -205,17 +179,9 @@ int merge_mode(int units)
 
 int env_pieces(int dflt)
 {
-    const char *e = std::getenv("SPMV_HW_PIECES");
+    const char *e = ablation_env("SPMV_HW_PIECES");
     return e ? std::max(1, std::atoi(e)) : dflt;
 }
-
-// one piece of accum_results' '+=': dst[i] += src[i] once `ready` (the copy of src) completed
-struct add_part {
-    ValueType *dst;
-    const ValueType *src;
-    uint64_t count;
-    hipEvent_t ready;
-};
 
 // Copies rows [0, rows) of a device y slice into pinned staging on stream s as `pieces` copies,
 // each followed by an event, and appends one add_part per piece (dst = the caller's y). The
@@ -240,64 +206,37 @@ void enqueue_d2h(ValueType *y_dst, ValueType *stage, const ValueType *d_src, uin
                   "hipMemcpyAsync(y)");
             check(hipEventRecord(done.get(t), s), "hipEventRecord");
         }
-        parts.push_back({y_dst + b, stage + b, e - b, done.get(pipe ? t : 0)});
+        parts.push_back({y_dst + b, stage + b, e - b, static_cast<void *>(done.get(pipe ? t : 0))});
     }
 }
 
-// adds the parts in on up to 16 host threads, in copy order: thread t adds the t-th sixteenth of
-// every part as soon as that part's copy has landed, so the adds run behind the DMA and the last
-// piece to land leaves 1/16 of a piece per thread (env SPMV_HW_ADD_SPLIT=0: thread t adds whole
-// parts t, t + 16, ... instead). Each thread first maps its ranges of the caller's y writable
-// (prefault, while the DMA runs). Returns when (timestamp_us) the last copy was seen complete.
-double host_accumulate(const std::vector<add_part> &parts)
+int wait_event(void *ready, std::string *err)
 {
-    const char *pf_env = std::getenv("SPMV_HW_PREFAULT");
-    const bool pf = !(pf_env && pf_env[0] == '0');  // 0: let the adds take the page faults
-    const char *se = std::getenv("SPMV_HW_ADD_SPLIT");
-    const bool split = !(se && se[0] == '0');
-    const char *te = std::getenv("SPMV_HW_ADD_THREADS");
-    uint64_t total = 0;
-    for (const add_part &q : parts)
-        total += q.count;
-    const size_t T = parts.empty() ? 0
-                     : total < (1u << 18) ? 1
-                     : std::min<size_t>(te ? std::max(1, std::atoi(te)) : 16, split ? size_t(64) : parts.size());
-    // thread t's range of part k: [b, e)
-    auto range = [&](size_t t, size_t k, uint64_t &b, uint64_t &e) {
-        const uint64_t n = parts[k].count;
-        if (split)
-            b = n * t / T, e = n * (t + 1) / T;
-        else
-            b = 0, e = k % T == t ? n : 0;
-    };
-    std::vector<double> landed(T, 0.0);
-    auto work = [&](size_t t) {
-        uint64_t b, e;
-        if (pf)
-            for (size_t k = 0; k < parts.size(); ++k) {
-                range(t, k, b, e);
-                if (e > b)
-                    prefault(parts[k].dst + b, e - b);
-            }
-        for (size_t k = 0; k < parts.size(); ++k) {
-            range(t, k, b, e);
-            if (e <= b)
-                continue;
-            const add_part &q = parts[k];
-            check(hipEventSynchronize(q.ready), "y copy");
-            landed[t] = timestamp_us();
-            for (uint64_t i = b; i < e; ++i)
-                q.dst[i] += q.src[i];
-        }
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < T; ++t)
-        th.emplace_back(work, t);
-    if (T)
-        work(0);
-    for (auto &t : th)
-        t.join();
-    return T ? *std::max_element(landed.begin(), landed.end()) : timestamp_us();
+    const hipError_t e = hipEventSynchronize(static_cast<hipEvent_t>(ready));
+    if (e != hipSuccess)
+        *err = std::string("y copy: ") + hipGetErrorString(e);
+    return e != hipSuccess;
+}
+
+// accum_results' '+=' of the landed pieces into the caller's y (spmv_host.hpp, host.cpp) on up
+// to 16 host threads; returns when (timestamp_us) the last copy was seen complete. The
+// documented knob SPMV_HW_PREFAULT=0 lets the adds take the page faults; the split and thread
+// count are switches of the tools build.
+double accumulate(const std::vector<add_part> &parts)
+{
+    accum_options o;
+    const char *pf = std::getenv("SPMV_HW_PREFAULT");
+    o.prefault = !(pf && pf[0] == '0');
+    const char *se = ablation_env("SPMV_HW_ADD_SPLIT");
+    o.split = !(se && se[0] == '0');
+    if (const char *te = ablation_env("SPMV_HW_ADD_THREADS"))
+        o.threads = std::max(1, std::atoi(te));
+    bool failed = false;
+    std::string err;
+    const double landed = host_accumulate(parts.data(), parts.size(), wait_event, o, &failed, &err);
+    if (failed)
+        die(err);
+    return landed;
 }
 
 }  // namespace
@@ -542,8 +481,8 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         if (trace) {
             double cms = 0, ems = 0;
             spmv_mgpu_get_timing(c->mg, &cms, &ems);
-            std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms (kernels %.3f, exchange %.3f)\n", "spmv_hw: RCCL merge",
-                         hw_exec, cms, ems);
+            std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms (kernels %.3f, exchange %.3f, %d RCCL calls)\n",
+                         "spmv_hw: RCCL merge", hw_exec, cms, ems, mgpu_rccl_calls(c->mg));
         }
         // one D2H copy of the whole y from GPU 0, then the host += (accum_results into y_fpga)
         const double ra_s = timestamp_us();
@@ -553,7 +492,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         if (c->rows)
             enqueue_d2h(y_fpga->values, c->h_full, mgpu_root_y(c->mg), c->rows, c->rows < (1u << 18) ? 1 : env_pieces(8),
                         unit_stream(0), c->done, parts);
-        const double landed = host_accumulate(parts);
+        const double landed = accumulate(parts);
         if (trace)
             std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "spmv_hw: D2H landed", (landed - ra_s) / 1000);
         tr("spmv_hw: D2H + host accumulation", ra_s);
@@ -607,7 +546,7 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
             }
     }
     tr("spmv_hw: D2H enqueue", ra_s);
-    const double landed = host_accumulate(parts);
+    const double landed = accumulate(parts);
     if (trace)
         std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "spmv_hw: D2H landed", (landed - ra_s) / 1000);
     tr("spmv_hw: host accumulation", ra_s);
@@ -669,42 +608,5 @@ void delete_csr_hw_y_vector(csr_hw_vector **hw_vector)
 
 // csr_hw_wrapper.cpp:305-308
 void delete_csr_hw_x_vector(csr_hw_vector *hw_vector) { delete_vector(hw_vector); }
-
-// csr_hw.cpp:1401-1409: MB of one unit's representation (computed in 64 bits)
-ValueType storage_overhead(csr_hw_matrix *matrix)
-{
-    if (!matrix)
-        return 0;
-    uint64_t bits = uint64_t(matrix->blocks) * 5 * INDEX_TYPE_BIT_WIDTH;
-    for (int b = 0; b < matrix->blocks; ++b)
-        bits += (uint64_t(matrix->nr_ci[b]) + matrix->nr_val[b]) * BUS_BIT_WIDTH;
-    return (ValueType)(bits / (8.0 * 1024 * 1024));
-}
-
-// csr_hw.cpp:1571-1590
-int verification(uint32_t nr_values, ValueType *sw_values, ValueType *hw_values, int verbose)
-{
-    const ValueType diff_thres = (ValueType)1e-5;
-    int status = 0;
-    IndexType err_cnt = 0;
-    for (IndexType i = 0; i < nr_values; ++i) {
-        const ValueType diff = std::fabs(sw_values[i] - hw_values[i]);
-        if (verbose == 2)
-            std::cout << std::setprecision(14) << i << " : y_gold = " << sw_values[i]
-                      << "\ty_hw = " << hw_values[i] << "\n";
-        if (diff >= diff_thres || diff != diff) {
-            status = 1;
-            ++err_cnt;
-            if (verbose == 1 || verbose == 2)
-                std::cout << std::setprecision(14) << "\tError occurs at " << i << " : y_gold = "
-                          << sw_values[i] << ", y_hw = " << hw_values[i]
-                          << ". Relative difference is " << std::fabs(diff / sw_values[i]) << "\n";
-        }
-    }
-    if (status)
-        std::cout << "Total errors : " << err_cnt << "\n";
-    std::cout.flush();
-    return status;
-}
 
 }  // extern "C"

@@ -48,6 +48,7 @@ struct Rccl {
     decltype(&ncclReduce) Reduce = nullptr;
     decltype(&ncclSend) Send = nullptr;
     decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclCommCount) CommCount = nullptr;
 };
 
 // first RCCL already in the process, else the ROCm one
@@ -82,9 +83,10 @@ const Rccl *rccl()
     SYM(Reduce);
     SYM(Send);
     SYM(Recv);
+    SYM(CommCount);
 #undef SYM
     if (!r.CommInitAll || !r.CommInitRank || !r.GetUniqueId || !r.CommDestroy || !r.GetErrorString || !r.GroupStart || !r.GroupEnd || !r.Broadcast ||
-        !r.Reduce || !r.Send || !r.Recv) {
+        !r.Reduce || !r.Send || !r.Recv || !r.CommCount) {
         r.h = nullptr;
         return nullptr;
     }
@@ -113,6 +115,7 @@ struct spmv_mgpu {
     std::vector<ValueType *> y;         // rank 0 only: the full y
     std::vector<hipEvent_t> ev;         // per device: start, kernels done, exchange done
     double compute_ms = 0, exchange_ms = 0;
+    int rccl_calls = 0;                 // RCCL calls (schedule exchange ops) the last run issued
     // spmv_mgpu_run_pipelined: per device a second stream for the exchange, a second y buffer
     // (and reduce partial), and the events that hand each buffer between the two streams
     struct Pipe {
@@ -211,6 +214,73 @@ struct spmv_mgpu {
             return 1;                                                                          \
         }                                                                                      \
     } while (0)
+
+// The buffers a schedule (spmv_mgpu_schedule, host.cpp) names, resolved for one device (and one
+// slot of the pipelined double buffer)
+struct XBufs {
+    ValueType *y, *slice, *part, *xnext;
+    ValueType *at(int buf) const
+    {
+        return buf == SPMV_XBUF_Y ? y : buf == SPMV_XBUF_SLICE ? slice : buf == SPMV_XBUF_PART ? part : xnext;
+    }
+};
+
+// the schedule of local device d's rank for one step
+static std::vector<spmv_xop> schedule_of(const spmv_mgpu *mg, int d, int exchange)
+{
+    std::vector<spmv_xop> ops(2 + 2 * size_t(mg->nranks));
+    const int n = spmv_mgpu_schedule(exchange, mg->rank[d], mg->nranks, mg->bounds.data(), ops.data(), (int)ops.size());
+    ops.resize(n < 0 ? 0 : std::min<size_t>(n, ops.size()));
+    return ops;
+}
+
+static bool has_exchange(const std::vector<spmv_xop> &ops)
+{
+    for (const spmv_xop &o : ops)
+        if (o.kind >= SPMV_XOP_SEND)
+            return true;
+    return false;
+}
+
+// the local ops (ZERO, COMPUTE) of device d on its compute stream s
+static int issue_local(spmv_mgpu *mg, int d, const std::vector<spmv_xop> &ops, const XBufs &b, const ValueType *x,
+                       hipStream_t s)
+{
+    for (const spmv_xop &o : ops) {
+        if (o.kind == SPMV_XOP_ZERO)
+            SPMV_TRY(hipMemsetAsync(b.at(o.buf) + o.offset, 0, size_t(o.count) * sizeof(ValueType), s));
+        else if (o.kind == SPMV_XOP_COMPUTE && spmv_plan_run(mg->plan[d], x, b.at(o.buf) + o.offset, s))
+            return 1;
+    }
+    return 0;
+}
+
+// the exchange ops of device d on stream s; the caller brackets every local device's calls with
+// one ncclGroupStart / ncclGroupEnd
+static int issue_exchange(spmv_mgpu *mg, int d, const std::vector<spmv_xop> &ops, const XBufs &b, hipStream_t s)
+{
+    for (const spmv_xop &o : ops) {
+        ValueType *p = b.at(o.buf) + o.offset;
+        switch (o.kind) {
+        case SPMV_XOP_SEND:
+            MG_NCCL(mg->nc->Send(p, o.count, kNcclValue, o.peer, mg->comm[d], s));
+            break;
+        case SPMV_XOP_RECV:
+            MG_NCCL(mg->nc->Recv(p, o.count, kNcclValue, o.peer, mg->comm[d], s));
+            break;
+        case SPMV_XOP_REDUCE:
+            MG_NCCL(mg->nc->Reduce(p, o.out >= 0 ? b.at(o.out) + o.offset : nullptr, o.count, kNcclValue, ncclSum, o.peer,
+                                   mg->comm[d], s));
+            break;
+        case SPMV_XOP_BCAST:
+            MG_NCCL(mg->nc->Broadcast(p, p, o.count, kNcclValue, o.peer, mg->comm[d], s));
+            break;
+        default:
+            break;
+        }
+    }
+    return 0;
+}
 
 extern "C" {
 
@@ -475,6 +545,8 @@ int mgpu_create_borrowed(spmv_mgpu **out, int n, const int *devices, const Index
     return 0;
 }
 
+int mgpu_rccl_calls(const spmv_mgpu *mg) { return mg->rccl_calls; }
+
 const ValueType *mgpu_root_y(const spmv_mgpu *mg)
 {
     const int r0 = mg->root_local();
@@ -492,7 +564,7 @@ int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev)
         set_error("spmv_mgpu_run: the all-gather exchange makes y the next x (needs a square matrix)");
         return 1;
     }
-    const int nl = mg->nloc, nr = mg->nranks;
+    const int nl = mg->nloc;
     const size_t nb = size_t(mg->nr_rows) * sizeof(ValueType);
     // buffers of the exchange form, allocated on first use
     for (int d = 0; d < nl; ++d) {
@@ -502,48 +574,29 @@ int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev)
         if (exchange == 2 && !mg->xnext[d])
             SPMV_TRY(hipMalloc((void **)&mg->xnext[d], std::max<size_t>(nb, sizeof(ValueType))));
     }
-    // where device d's kernels write its rows
-    auto dst = [&](int d) -> ValueType * {
-        const IndexType b = mg->bounds[mg->rank[d]];
-        if (exchange == 2)
-            return mg->xnext[d] + b;
-        if (exchange == 1)
-            return mg->ypart[d] + b;
-        return mg->rank[d] == 0 ? mg->y[d] + b : mg->yslice[d];
-    };
+    std::vector<std::vector<spmv_xop>> sch(nl);
+    bool any = false;
+    for (int d = 0; d < nl; ++d) {
+        sch[d] = schedule_of(mg, d, exchange);
+        any = any || has_exchange(sch[d]);
+    }
+    auto bufs = [&](int d) { return XBufs{mg->y[d], mg->yslice[d], mg->ypart[d], mg->xnext[d]}; };
     for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         hipStream_t s = mg->stream[d];
         SPMV_TRY(hipEventRecord(mg->ev[3 * d], s));
-        if (exchange == 1)  // full-length partial: zero outside the slice
-            SPMV_TRY(hipMemsetAsync(mg->ypart[d], 0, nb, s));
-        if (mg->rows(d) && spmv_plan_run(mg->plan[d], x_dev ? x_dev[d] : mg->x[d], dst(d), s))
+        if (issue_local(mg, d, sch[d], bufs(d), x_dev ? x_dev[d] : mg->x[d], s))
             return 1;
         SPMV_TRY(hipEventRecord(mg->ev[3 * d + 1], s));
     }
-    // a reduce runs on one rank too (RCCL copies the partial into y): the same code path as N
-    if ((nr > 1 || exchange == 1) && mg->nr_rows) {
+    mg->rccl_calls = 0;
+    if (any) {
         MG_NCCL(mg->nc->GroupStart());
         for (int d = 0; d < nl; ++d) {
-            hipStream_t s = mg->stream[d];
-            const int rk = mg->rank[d];
-            if (exchange == 0) {
-                if (rk == 0) {
-                    for (int p = 1; p < nr; ++p)
-                        if (mg->rows_of(p))
-                            MG_NCCL(mg->nc->Recv(mg->y[d] + mg->bounds[p], mg->rows_of(p), kNcclValue, p, mg->comm[d], s));
-                } else if (mg->rows(d)) {
-                    MG_NCCL(mg->nc->Send(mg->yslice[d], mg->rows(d), kNcclValue, 0, mg->comm[d], s));
-                }
-            } else if (exchange == 1) {
-                MG_NCCL(mg->nc->Reduce(mg->ypart[d], rk == 0 ? mg->y[d] : nullptr, mg->nr_rows, kNcclValue, ncclSum, 0,
-                                       mg->comm[d], s));
-            } else {
-                for (int r = 0; r < nr; ++r)  // slice r from its owner into every device's next x
-                    if (mg->rows_of(r))
-                        MG_NCCL(mg->nc->Broadcast(mg->xnext[d] + mg->bounds[r], mg->xnext[d] + mg->bounds[r],
-                                                  mg->rows_of(r), kNcclValue, r, mg->comm[d], s));
-            }
+            if (issue_exchange(mg, d, sch[d], bufs(d), mg->stream[d]))
+                return 1;
+            for (const spmv_xop &o : sch[d])
+                mg->rccl_calls += o.kind >= SPMV_XOP_SEND;
         }
         MG_NCCL(mg->nc->GroupEnd());
     }
@@ -596,7 +649,7 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
         set_error("spmv_mgpu_run_pipelined: bad arguments (gather or reduce, steps >= 1)");
         return 1;
     }
-    const int nl = mg->nloc, nr = mg->nranks;
+    const int nl = mg->nloc;
     const bool red = exchange == SPMV_MGPU_REDUCE;
     const size_t nb = size_t(mg->nr_rows) * sizeof(ValueType);
     if (mg->pipe.empty())
@@ -621,16 +674,17 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
         if (red && !q.part2)
             SPMV_TRY(hipMalloc((void **)&q.part2, std::max<size_t>(nb, sizeof(ValueType))));
     }
-    // buffer b of device d: where its kernels write, and what the exchange sends / receives into
-    auto out = [&](int d, int b) -> ValueType * {  // rank 0's full y (gather and reduce output)
-        return b == 0 ? mg->y[d] : mg->pipe[d].buf2;
+    // buffer set b of device d: the handle's own buffers (b = 0) or the pipeline's second ones
+    auto bufs = [&](int d, int b) {
+        spmv_mgpu::Pipe &q = mg->pipe[d];
+        return b == 0 ? XBufs{mg->y[d], mg->yslice[d], mg->ypart[d], nullptr} : XBufs{q.buf2, q.buf2, q.part2, nullptr};
     };
-    auto slice = [&](int d, int b) -> ValueType * {  // gather, rank > 0: its rows
-        return b == 0 ? mg->yslice[d] : mg->pipe[d].buf2;
-    };
-    auto part = [&](int d, int b) -> ValueType * {  // reduce: full-length partial
-        return b == 0 ? mg->ypart[d] : mg->pipe[d].part2;
-    };
+    std::vector<std::vector<spmv_xop>> sch(nl);
+    bool any = false;
+    for (int d = 0; d < nl; ++d) {
+        sch[d] = schedule_of(mg, d, exchange);
+        any = any || has_exchange(sch[d]);
+    }
     for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         SPMV_TRY(hipEventRecord(mg->pipe[d].t0, mg->stream[d]));
@@ -643,34 +697,16 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
             hipStream_t s = mg->stream[d];
             if (k >= 2)  // buffer b is free once the exchange of step k - 2 completed
                 SPMV_TRY(hipStreamWaitEvent(s, q.exch[b], 0));
-            ValueType *dst;
-            if (red) {
-                SPMV_TRY(hipMemsetAsync(part(d, b), 0, nb, s));
-                dst = part(d, b) + mg->bounds[mg->rank[d]];
-            } else {
-                dst = mg->rank[d] == 0 ? out(d, b) + mg->bounds[0] : slice(d, b);
-            }
-            if (mg->rows(d) && spmv_plan_run(mg->plan[d], mg->x[d], dst, s))
+            if (issue_local(mg, d, sch[d], bufs(d, b), mg->x[d], s))
                 return 1;
             SPMV_TRY(hipEventRecord(q.comp[b], s));
             SPMV_TRY(hipStreamWaitEvent(q.cs, q.comp[b], 0));
         }
-        if ((nr > 1 || red) && mg->nr_rows) {
+        if (any) {
             MG_NCCL(mg->nc->GroupStart());
-            for (int d = 0; d < nl; ++d) {
-                hipStream_t cs = mg->pipe[d].cs;
-                const int rk = mg->rank[d];
-                if (red) {
-                    MG_NCCL(mg->nc->Reduce(part(d, b), rk == 0 ? out(d, b) : nullptr, mg->nr_rows, kNcclValue, ncclSum,
-                                           0, mg->comm[d], cs));
-                } else if (rk == 0) {
-                    for (int p = 1; p < nr; ++p)
-                        if (mg->rows_of(p))
-                            MG_NCCL(mg->nc->Recv(out(d, b) + mg->bounds[p], mg->rows_of(p), kNcclValue, p, mg->comm[d], cs));
-                } else if (mg->rows(d)) {
-                    MG_NCCL(mg->nc->Send(slice(d, b), mg->rows(d), kNcclValue, 0, mg->comm[d], cs));
-                }
-            }
+            for (int d = 0; d < nl; ++d)
+                if (issue_exchange(mg, d, sch[d], bufs(d, b), mg->pipe[d].cs))
+                    return 1;
             MG_NCCL(mg->nc->GroupEnd());
         }
         for (int d = 0; d < nl; ++d) {
@@ -693,10 +729,15 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
         tmax = std::max(tmax, (double)t);
         SPMV_TRY(hipStreamSynchronize(mg->stream[d]));
     }
-    if ((steps - 1) & 1)  // the last result sits in the second buffers: make them rank 0's y
+    // the last result sits in the second buffers: copy it into rank 0's y, so y keeps its address
+    // (pointers from spmv_mgpu_y_device and graphs captured by spmv_mgpu_run_graph stay valid)
+    if ((steps - 1) & 1)
         for (int d = 0; d < nl; ++d)
-            if (mg->rank[d] == 0)
-                std::swap(mg->y[d], mg->pipe[d].buf2);
+            if (mg->rank[d] == 0 && mg->nr_rows) {
+                SPMV_TRY(hipSetDevice(mg->dev[d]));
+                SPMV_TRY(hipMemcpyAsync(mg->y[d], mg->pipe[d].buf2, nb, hipMemcpyDeviceToDevice, mg->stream[d]));
+                SPMV_TRY(hipStreamSynchronize(mg->stream[d]));
+            }
     if (ms_per_step)
         *ms_per_step = tmax / steps;
     return 0;
@@ -707,33 +748,14 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
 // RCCL calls only)
 static int enqueue_step(spmv_mgpu *mg, int exchange, const ValueType *x_in, ValueType *x_out, hipStream_t s)
 {
-    const int rk = mg->rank[0], nr = mg->nranks;
-    const size_t nb = size_t(mg->nr_rows) * sizeof(ValueType);
-    const IndexType b0 = mg->bounds[rk];
-    ValueType *dst = exchange == 2 ? x_out + b0 : exchange == 1 ? mg->ypart[0] + b0 : rk == 0 ? mg->y[0] + b0 : mg->yslice[0];
-    if (exchange == 1)
-        SPMV_TRY(hipMemsetAsync(mg->ypart[0], 0, nb, s));
-    if (mg->rows(0) && spmv_plan_run(mg->plan[0], x_in, dst, s))
+    const std::vector<spmv_xop> ops = schedule_of(mg, 0, exchange);
+    const XBufs b{mg->y[0], mg->yslice[0], mg->ypart[0], x_out};
+    if (issue_local(mg, 0, ops, b, x_in, s))
         return 1;
-    if ((nr > 1 || exchange == 1) && mg->nr_rows) {
+    if (has_exchange(ops)) {
         MG_NCCL(mg->nc->GroupStart());
-        if (exchange == 0) {
-            if (rk == 0) {
-                for (int p = 1; p < nr; ++p)
-                    if (mg->rows_of(p))
-                        MG_NCCL(mg->nc->Recv(mg->y[0] + mg->bounds[p], mg->rows_of(p), kNcclValue, p, mg->comm[0], s));
-            } else if (mg->rows(0)) {
-                MG_NCCL(mg->nc->Send(mg->yslice[0], mg->rows(0), kNcclValue, 0, mg->comm[0], s));
-            }
-        } else if (exchange == 1) {
-            MG_NCCL(mg->nc->Reduce(mg->ypart[0], rk == 0 ? mg->y[0] : nullptr, mg->nr_rows, kNcclValue, ncclSum, 0,
-                                   mg->comm[0], s));
-        } else {
-            for (int r = 0; r < nr; ++r)
-                if (mg->rows_of(r))
-                    MG_NCCL(mg->nc->Broadcast(x_out + mg->bounds[r], x_out + mg->bounds[r], mg->rows_of(r), kNcclValue, r,
-                                              mg->comm[0], s));
-        }
+        if (issue_exchange(mg, 0, ops, b, s))
+            return 1;
         MG_NCCL(mg->nc->GroupEnd());
     }
     return 0;
@@ -871,6 +893,16 @@ int spmv_mgpu_slice(const spmv_mgpu *mg, int r, IndexType *row_begin, IndexType 
             if (mg->rank[d] == r)
                 *device = mg->dev[d];
     }
+    return 0;
+}
+
+int spmv_mgpu_comm_count(const spmv_mgpu *mg, int *count)
+{
+    if (!mg || !count || !mg->comm[0]) {
+        set_error("spmv_mgpu_comm_count: bad arguments");
+        return 1;
+    }
+    MG_NCCL(mg->nc->CommCount(mg->comm[0], count));
     return 0;
 }
 

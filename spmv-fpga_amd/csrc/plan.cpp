@@ -22,10 +22,6 @@ static int run_impl(spmv_plan *p, const ValueType *d_x, ValueType *d_y, hipStrea
 
 namespace spmvhw {
 
-static thread_local std::string g_err;
-void set_error(const std::string &msg) { g_err = msg; }
-const char *get_error() { return g_err.c_str(); }
-
 // Host -> device copy of a pageable buffer through two pinned 32 MiB staging buffers (process
 // lifetime): host threads fill one buffer while the DMA engine drains the other. A pageable
 // hipMemcpy runs at ~1 GB/s here; this keeps the PCIe link busy instead.
@@ -228,11 +224,11 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
         SPMV_TRY(hipMemcpyAsync(p.d_cross, cross.data(), cross.size() * 4, hipMemcpyHostToDevice, s));
     if (p.nnz_pad)
         SPMV_TRY(launch_pack(d_col_src, d_val_src, nnz, p.nnz_pad, p.nr_cols, p.d_col, p.d_val, nullptr, s));
-    if (const char *xe = std::getenv("SPMV_TILE_XCD"))
+    if (const char *xe = ablation_env("SPMV_TILE_XCD"))
         p.tile_xcd = xe[0] == '1';
     // narrow form: 8- or 16-bit column offsets from a per-tile base when every tile allows it
     // (env SPMV_TILE_NARROW: 0 = keep 32-bit columns, 16 = at most 16-bit, default narrowest)
-    const char *nenv = std::getenv("SPMV_TILE_NARROW");
+    const char *nenv = ablation_env("SPMV_TILE_NARROW");
     const int narrow_min = !nenv || !*nenv ? 1 : std::atoi(nenv) == 16 ? 2 : std::atoi(nenv) == 0 ? 4 : 1;
     if (p.ntiles && narrow_min < 4) {
         uint32_t *d_span = nullptr;
@@ -260,7 +256,7 @@ static int build_tiles(spmv_plan &p, const IndexType *h_row_ptr, const IndexType
             SPMV_TRY(hipFree(p.d_tile_cbase));
             p.d_tile_cbase = nullptr;
             // clustered 16-bit columns: up to four narrow column clusters per tile
-            const char *cenv = std::getenv("SPMV_TILE_CLUSTER");
+            const char *cenv = ablation_env("SPMV_TILE_CLUSTER");
             if (!(cenv && cenv[0] == '0')) {
                 uint32_t *d_bad = nullptr;
                 SPMV_TRY(alloc((void **)&p.d_tile_cbase, p.ntiles * 4 * sizeof(uint32_t)));
@@ -538,7 +534,7 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             kernel = kKernelBinned;
     }
     trace("validate + kernel choice", s);
-    if (const char *t = std::getenv("SPMV_SWEEP_THREADS")) {
+    if (const char *t = ablation_env("SPMV_SWEEP_THREADS")) {
         const int v = std::atoi(t);
         if (v == 256 || v == 512 || v == 1024)
             p->sweep_threads = v;
@@ -698,9 +694,6 @@ uint64_t spmv_plan::algorithmic_bytes() const
 }
 
 extern "C" {
-
-const char *spmv_hw_last_error(void) { return get_error(); }
-int spmv_hw_value_bytes(void) { return (int)sizeof(ValueType); }
 
 int spmv_plan_create_device(spmv_plan **plan, int device, IndexType nr_rows, IndexType nr_cols,
                             IndexType nr_nzeros, const IndexType *d_row_ptr,
@@ -985,24 +978,5 @@ int spmv_plan_get_timing(spmv_plan *p, double *mean_ms, double *total_ms, int *l
 }
 
 void spmv_plan_destroy(spmv_plan *p) { delete p; }
-
-int spmv_partition_rows(const IndexType *row_ptr, IndexType nr_rows, int units, IndexType *bounds)
-{
-    if (!row_ptr || !bounds || units < 1) {
-        set_error("spmv_partition_rows: bad arguments");
-        return 1;
-    }
-    const uint64_t nnz = uint64_t(row_ptr[nr_rows]) - row_ptr[0];
-    bounds[0] = 0;
-    for (int u = 1; u < units; ++u) {
-        const uint64_t target = row_ptr[0] + nnz * uint64_t(u) / uint64_t(units);
-        // first row whose start is >= target
-        const IndexType *it = std::lower_bound(row_ptr, row_ptr + nr_rows, (IndexType)target);
-        IndexType b = (IndexType)(it - row_ptr);
-        bounds[u] = std::max(b, bounds[u - 1]);
-    }
-    bounds[units] = nr_rows;
-    return 0;
-}
 
 }  // extern "C"

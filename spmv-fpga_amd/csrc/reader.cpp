@@ -35,7 +35,7 @@
 #include <thread>
 #include <vector>
 
-#include "spmv_internal.hpp"
+#include "spmv_host.hpp"
 
 namespace {
 

@@ -441,7 +441,7 @@ int build_slices(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         p.slice_acc_native = sizeof(ValueType) == 4 && aenv && std::atoi(aenv) == 32;
     }
     // env SPMV_SLICE_NARROW=0 keeps 32-bit columns
-    const char *nenv = std::getenv("SPMV_SLICE_NARROW");
+    const char *nenv = ablation_env("SPMV_SLICE_NARROW");
     const bool narrow = !(nenv && nenv[0] == '0');
     int ob = !narrow ? 4 : span < 256u ? 1 : span < 65536u ? 2 : 4;
     if (ob == 4 && narrow && n) {  // try up to 4 clusters of 16384 columns per slot

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "csr_hw_wrapper.h"
+#include "spmv_host.hpp"
 
 namespace spmvhw {
 
@@ -207,9 +208,6 @@ struct spmv_plan {
 
 namespace spmvhw {
 
-void set_error(const std::string &msg);
-const char *get_error();
-
 // Launch, or (warm) only have the runtime load the kernel's code object: plan creation runs the
 // launchers warm so that the first SpMV of a plan does not pay the lazy module load (~8 ms).
 template <typename K, typename... Args>
@@ -284,6 +282,7 @@ int mgpu_create_borrowed(spmv_mgpu **out, int n, const int *devices, const Index
                          const spmv_plan *const *plans);
 int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev);
 const ValueType *mgpu_root_y(const spmv_mgpu *mg);
+int mgpu_rccl_calls(const spmv_mgpu *mg);  // RCCL calls the last mgpu_run_on issued
 }  // namespace spmvhw
 
 #define SPMV_TRY(expr)                                                                        \

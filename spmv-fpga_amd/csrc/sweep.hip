@@ -1078,7 +1078,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     // a workgroup of T threads gets T/1024 of one CU's LDS for its panel's y
     const uint64_t lds_bytes = kSweepLdsBytes * p.sweep_threads / 1024 - 256;  // 256 B: static LDS
     // accumulator: fp64, or fp32 (compare-and-swap adds) for fp32 matrices with env SPMV_SWEEP_ACC=32
-    const char *aenv = std::getenv("SPMV_SWEEP_ACC");
+    const char *aenv = ablation_env("SPMV_SWEEP_ACC");
     p.sweep_acc_bytes = sizeof(ValueType) == 4 && aenv && std::atoi(aenv) == 32 ? 4 : 8;
     const uint64_t acc = p.sweep_acc_bytes;
     const uint32_t rmax = (uint32_t)std::min<uint64_t>(lds_bytes / acc - 1, 65534);
@@ -1091,7 +1091,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     const int chip_cus = cus;
     cus *= 1024 / p.sweep_threads;  // resident workgroups per round
     // env SPMV_SWEEP_SPLIT: 0 = never split, 2 = split whenever >= 2 pieces fit, else heuristic
-    const char *senv = std::getenv("SPMV_SWEEP_SPLIT");
+    const char *senv = ablation_env("SPMV_SWEEP_SPLIT");
     // env SPMV_SWEEP_DETERMINISTIC=1: the same layout, run by k_spmv_sweep_turn (ordered adds)
     const char *denv = std::getenv("SPMV_SWEEP_DETERMINISTIC");
     const bool det = denv && denv[0] == '1';
@@ -1186,7 +1186,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     // further, so that no workgroup gets more than ~2x the mean work
     uint32_t split = split_mode ? std::max<uint32_t>(1, (uint32_t)cus / P) : 1;
     // env SPMV_SWEEP_PIECES=k (experiments): k pieces per panel in split mode instead of cus / P
-    if (const char *kenv = std::getenv("SPMV_SWEEP_PIECES"); split_mode && kenv && std::atoi(kenv) > 0)
+    if (const char *kenv = ablation_env("SPMV_SWEEP_PIECES"); split_mode && kenv && std::atoi(kenv) > 0)
         split = (uint32_t)std::atoi(kenv);
     const double mean = P ? double(padded) / P : 0.0;
     std::vector<uint32_t> punit(P + 1, 0);
@@ -1226,7 +1226,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         // launch all finish together, and each last arriver then reads its 4 x 160 KiB of partials
         // alone (~50-70 GB/s per workgroup, MI355X_MICROARCH.md handoff-payload) where the combine
         // kernel reads them with the whole chip; so the separate launch stays the default
-        const char *cenv = std::getenv("SPMV_SWEEP_COMBINE");
+        const char *cenv = ablation_env("SPMV_SWEEP_COMBINE");
         if (cenv && std::strcmp(cenv, "fused") == 0) {
             SPMV_TRY(hipMalloc((void **)&p.d_panel_cnt, std::max<uint64_t>(P, 1) * 4));
             SPMV_TRY(hipMemsetAsync(p.d_panel_cnt, 0, std::max<uint64_t>(P, 1) * 4, s));
@@ -1319,7 +1319,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         uint32_t bad = 0;
         SW_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
         SW_TRY(hipStreamSynchronize(s));
-        const char *env = std::getenv("SPMV_SWEEP_PACKED");
+        const char *env = ablation_env("SPMV_SWEEP_PACKED");
         const bool want = !(env && env[0] == '0');
         if (!bad && want && p.ent_pad) {
             hipLaunchKernelGGL(k_sweep_pack_rc, dim3((unsigned)((p.ent_pad + 255) / 256)), dim3(256), 0, s, p.d_s_col,
@@ -1329,7 +1329,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             SW_TRY(hipFree(p.d_s_row));
             p.d_s_row = nullptr;
             p.sweep_packed = true;
-            const char *lo = std::getenv("SPMV_SWEEP_LANE_ORDER");
+            const char *lo = ablation_env("SPMV_SWEEP_LANE_ORDER");
             if (!(lo && lo[0] == '0')) {
                 uint32_t *rc2 = nullptr;
                 ValueType *v2 = nullptr;

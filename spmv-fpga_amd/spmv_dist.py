@@ -119,6 +119,47 @@ def pipelined_gather(run_step, y_bufs, counts, steps: int, dst: int = 0):
     return torch.cat([last[r][:int(counts[r])] for r in range(world)])
 
 
+def execute_schedule(ops, bufs, compute):
+    """Runs one rank's step schedule (spmv_mgpu_schedule: the list every RCCL call of the
+    library's exchange iterates over, mgpu.cpp issue_local / issue_exchange) over
+    torch.distributed, op for op: ZERO and COMPUTE locally (compute(view) writes this rank's rows
+    of A x into `view`), then SEND / RECV as posted point-to-point operations (the RCCL group posts
+    them together), REDUCE and BCAST as collectives in list order (every rank lists them in the
+    same order). `bufs` maps an SPMV_XBUF_* id to this rank's 1-D tensor of that role. gloo runs it
+    on host tensors: the CPU replay of the multi-GPU merge (tests/test_exchange_schedule.py)."""
+    import spmv_hw as hw
+    for o in ops:
+        view = bufs[o["buf"]][o["offset"]:o["offset"] + o["count"]] if o["buf"] in bufs else None
+        if o["kind"] == hw.XOP_ZERO:
+            view.zero_()
+        elif o["kind"] == hw.XOP_COMPUTE:
+            compute(view)
+    pending = []
+    for o in ops:
+        k = o["kind"]
+        if k < hw.XOP_SEND:
+            continue
+        view = bufs[o["buf"]][o["offset"]:o["offset"] + o["count"]]
+        if k == hw.XOP_SEND:
+            pending.append((dist.isend(_staged(view).contiguous(), dst=o["peer"]), None, None))
+        elif k == hw.XOP_RECV:
+            tmp = torch.empty(o["count"], dtype=view.dtype, device="cpu" if dist.get_backend() == "gloo" else view.device)
+            pending.append((dist.irecv(tmp, src=o["peer"]), tmp, view))
+        elif k == hw.XOP_REDUCE:
+            tmp = _staged(view).clone()
+            dist.reduce(tmp, dst=o["peer"], op=dist.ReduceOp.SUM)
+            if o["out"] >= 0:
+                bufs[o["out"]][o["offset"]:o["offset"] + o["count"]].copy_(tmp)
+        elif k == hw.XOP_BCAST:
+            tmp = _staged(view).clone()
+            dist.broadcast(tmp, src=o["peer"])
+            view.copy_(tmp)
+    for work, tmp, view in pending:
+        work.wait()
+        if tmp is not None:
+            view.copy_(tmp)
+
+
 def broadcast_x(x: torch.Tensor, src: int = 0) -> torch.Tensor:
     """x replicated from rank `src` to every rank (broadcast once, then resident)."""
     buf = _staged(x)

@@ -29,11 +29,17 @@ _LIBS: dict = {}
 IndexType = ctypes.c_uint32
 
 
-def lib_path(dtype=np.float64) -> str:
-    """The product library; env SPMV_HW_ABLATIONS=1 selects the tools-only build with the
-    measurement-only kernel ablations (`make -C spmv-fpga_amd ablations`, tools/ab_variants.py)."""
+def ablations_requested() -> bool:
+    return os.environ.get("SPMV_HW_ABLATIONS") == "1"
+
+
+def lib_path(dtype=np.float64, ablations: bool | None = None) -> str:
+    """The product library; ablations=True (default: env SPMV_HW_ABLATIONS=1) selects the tools
+    build (`make -C spmv-fpga_amd ablations`, -DSPMV_ABLATIONS): the same kernels plus the
+    measurement-only variants and the environment switches that force layouts and schedules
+    (tools/ab_variants.py, and the tests that cover those layouts)."""
     name = {8: "libspmv_hw_f64.so", 4: "libspmv_hw_f32.so"}[np.dtype(dtype).itemsize]
-    if os.environ.get("SPMV_HW_ABLATIONS") == "1":
+    if ablations_requested() if ablations is None else ablations:
         return os.path.join(LIBDIR, "ablations", name)
     return os.path.join(LIBDIR, name)
 
@@ -105,18 +111,28 @@ EXPORTS = [
     "spmv_mgpu_create", "spmv_mgpu_set_x", "spmv_mgpu_run", "spmv_mgpu_get_y", "spmv_mgpu_get_timing",
     "spmv_mgpu_slice", "spmv_mgpu_destroy", "spmv_mgpu_unique_id", "spmv_mgpu_create_rank",
     "spmv_mgpu_set_x_device", "spmv_mgpu_set_x_device_on", "spmv_mgpu_y_device", "spmv_mgpu_run_pipelined",
-    "spmv_mgpu_run_graph",
+    "spmv_mgpu_run_graph", "spmv_mgpu_comm_count", "spmv_mgpu_schedule",
 ]
 
 MGPU_GATHER, MGPU_REDUCE, MGPU_ALLGATHER = 0, 1, 2  # include/csr_hw_wrapper.h SPMV_MGPU_*
+# spmv_xop kinds and buffers (include/csr_hw_wrapper.h SPMV_XOP_* / SPMV_XBUF_*)
+XOP_ZERO, XOP_COMPUTE, XOP_SEND, XOP_RECV, XOP_REDUCE, XOP_BCAST = range(6)
+XOP_NAMES = {XOP_ZERO: "zero", XOP_COMPUTE: "compute", XOP_SEND: "send", XOP_RECV: "recv",
+             XOP_REDUCE: "reduce", XOP_BCAST: "bcast"}
+XBUF_Y, XBUF_SLICE, XBUF_PART, XBUF_XNEXT = range(4)
+
+
+class spmv_xop(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("buf", ctypes.c_int32), ("peer", ctypes.c_int32),
+                ("out", ctypes.c_int32), ("offset", ctypes.c_uint32), ("count", ctypes.c_uint32)]
 
 
 class Lib:
     """Typed handle on one precision of libspmv_hw."""
 
-    def __init__(self, dtype=np.float64):
+    def __init__(self, dtype=np.float64, ablations: bool | None = None):
         self.dtype = np.dtype(dtype)
-        path = lib_path(self.dtype)
+        self.path = path = lib_path(self.dtype, ablations)
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is not built (run `make -C spmv-fpga_amd`); "
                                "the MI355X path has no CPU fallback")
@@ -182,6 +198,9 @@ class Lib:
             "spmv_mgpu_run_pipelined": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
             "spmv_mgpu_run_graph": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
             "spmv_mgpu_y_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp)]),
+            "spmv_mgpu_comm_count": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
+            "spmv_mgpu_schedule": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, up,
+                                                  ctypes.POINTER(spmv_xop), ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -302,6 +321,19 @@ class Lib:
                  "spmv_partition_rows")
         return bounds
 
+    def mgpu_schedule(self, exchange: int, rank: int, nranks: int, bounds):
+        """spmv_mgpu_schedule: the ops rank `rank` issues for one SpMV step (host only), as dicts
+        {kind, buf, peer, out, offset, count} in issue order."""
+        b = np.ascontiguousarray(bounds, np.uint32)
+        assert len(b) == nranks + 1
+        bp = b.ctypes.data_as(ctypes.POINTER(IndexType))
+        n = self.L.spmv_mgpu_schedule(int(exchange), int(rank), int(nranks), bp, None, 0)
+        if n < 0:
+            raise RuntimeError(f"spmv_mgpu_schedule: {self.L.spmv_hw_last_error().decode()}")
+        ops = (spmv_xop * max(n, 1))()
+        assert self.L.spmv_mgpu_schedule(int(exchange), int(rank), int(nranks), bp, ops, n) == n
+        return [{k: getattr(ops[i], k) for k, _ in spmv_xop._fields_} for i in range(n)]
+
     def powerlaw_row_ptr(self, n: int, nnz: int, max_len: int = 65536, seed: int = 4):
         rp = np.zeros(n + 1, np.uint32)
         s = ctypes.c_double()
@@ -413,6 +445,11 @@ class MultiGpu:
         """Every rank calls it; x (a device tensor) is read on rank 0 only. The copy is ordered
         after the torch stream that produced x (`stream`, default: the current stream) by an
         event, with no host wait."""
+        if x is not None:
+            # the C side records the producer event on rank 0's device: x must live there
+            dev0 = self.slice(0)[2]
+            if dev0 >= 0 and x.device.index != dev0:
+                raise ValueError(f"set_x_device: x is on cuda:{x.device.index}, rank 0 of this handle on cuda:{dev0}")
         if stream is None and x is not None:
             import torch
             stream = torch.cuda.current_stream(x.device)
@@ -434,6 +471,12 @@ class MultiGpu:
         self.lib._ok(self.lib.L.spmv_mgpu_run_graph(self.h, int(exchange), int(iters), ctypes.byref(ms)),
                      "spmv_mgpu_run_graph")
         return float(ms.value)
+
+    def comm_count(self) -> int:
+        """Ranks in the handle's RCCL communicator (ncclCommCount)."""
+        c = ctypes.c_int()
+        self.lib._ok(self.lib.L.spmv_mgpu_comm_count(self.h, ctypes.byref(c)), "spmv_mgpu_comm_count")
+        return int(c.value)
 
     def y_device_ptr(self, exchange: int = MGPU_GATHER) -> int:
         p = ctypes.c_void_p()
@@ -516,8 +559,10 @@ def _torch_dtype(dtype):
     return torch.float64 if np.dtype(dtype) == np.float64 else torch.float32
 
 
-def load(dtype=np.float64) -> Lib:
-    key = np.dtype(dtype).str
+def load(dtype=np.float64, ablations: bool | None = None) -> Lib:
+    """The library of `dtype`; the tools build when ablations (default: env SPMV_HW_ABLATIONS=1)."""
+    abl = ablations_requested() if ablations is None else bool(ablations)
+    key = (np.dtype(dtype).str, abl)
     if key not in _LIBS:
-        _LIBS[key] = Lib(dtype)
+        _LIBS[key] = Lib(dtype, abl)
     return _LIBS[key]

@@ -48,3 +48,22 @@ def golden_arrays(name, tag):
 
 FIXTURES = sorted(manifest().keys())
 DTYPES = [(np.float64, "f64"), (np.float32, "f32")]
+
+
+# environment switches read only by the tools build (make -C spmv-fpga_amd ablations,
+# -DSPMV_ABLATIONS; csrc/spmv_host.hpp ablation_env): they force layouts and schedules the
+# automatic choice takes on other matrices, or that were measured and not kept. The product
+# library ignores them (tests/test_abi.py checks which switches it reads).
+TOOLS_ONLY_ENV = ("SPMV_TILE_XCD", "SPMV_TILE_NARROW", "SPMV_TILE_CLUSTER", "SPMV_SWEEP_THREADS",
+                  "SPMV_BIN_XCC_BIAS", "SPMV_BIN_DELTA", "SPMV_BIN_PROD_SKEW", "SPMV_SLICE_NARROW",
+                  "SPMV_SWEEP_ACC", "SPMV_SWEEP_SPLIT", "SPMV_SWEEP_PIECES", "SPMV_SWEEP_COMBINE",
+                  "SPMV_SWEEP_PACKED", "SPMV_SWEEP_LANE_ORDER", "SPMV_HW_BLOCKING_SYNC",
+                  "SPMV_HW_PIECES", "SPMV_HW_ADD_SPLIT", "SPMV_HW_ADD_THREADS")
+
+
+def tools_env(monkeypatch, name, value):
+    """Sets a tools-only switch and selects the tools build for the libraries this test loads
+    (spmv_hw.load with env SPMV_HW_ABLATIONS=1): the same kernels, plus the switch."""
+    assert name in TOOLS_ONLY_ENV, name
+    monkeypatch.setenv(name, value)
+    monkeypatch.setenv("SPMV_HW_ABLATIONS", "1")

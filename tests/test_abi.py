@@ -281,3 +281,43 @@ def test_deterministic_kernel_ships_only_its_ordered_forms(dtype):
     assert turns
     ords = {ln.split("k_spmv_sweep_turn<", 1)[1].split(">", 1)[0].split(", ")[4] for ln in turns}
     assert ords == {"0", "1"}, ords
+
+
+DOCUMENTED_ENV = {"SPMV_NGPUS", "SPMV_HW_MERGE", "SPMV_HW_KERNEL", "SPMV_FPGA_VF", "SPMV_FPGA_BLOCK",
+                  "SPMV_SLICE_ACC", "SPMV_SWEEP_DETERMINISTIC", "SPMV_SWEEP_DELTA", "SPMV_SWEEP_XCC_BIAS",
+                  "SPMV_BIN_ROW_LIMIT", "SPMV_READ_THREADS", "SPMV_HW_TRACE", "SPMV_HW_PREFAULT",
+                  "SPMV_HW_PIPELINE"}
+
+
+def test_product_reads_only_the_documented_switches():
+    """outside the tools build (ablation_env, -DSPMV_ABLATIONS) the library reads
+    exactly the environment switches INTEGRATION.md documents; the tools-only ones are read
+    through ablation_env only, and INTEGRATION.md names every product switch."""
+    from conftest import TOOLS_ONLY_ENV
+    csrc = os.path.join(ROOT, "spmv-fpga_amd", "csrc")
+    direct, tools = set(), set()
+    for f in os.listdir(csrc):
+        text = open(os.path.join(csrc, f)).read()
+        direct |= set(re.findall(r'std::getenv\("([A-Z0-9_]+)"\)', text))
+        tools |= set(re.findall(r'ablation_env\("([A-Z0-9_]+)"\)', text))
+        # the one getenv of ablation_env itself sits under #ifdef SPMV_ABLATIONS
+        for m in re.finditer(r"\bgetenv\((?!\")", text):
+            head = text[:m.start()]
+            assert head.rfind("#ifdef SPMV_ABLATIONS") > head.rfind("#endif"), f
+    assert direct == DOCUMENTED_ENV
+    assert tools == set(TOOLS_ONLY_ENV)
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert all(f"`{k}" in doc for k in DOCUMENTED_ENV)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_product_library_carries_no_tools_only_switch_names(dtype):
+    """The product build drops the tools-only switch names altogether (ablation_env returns null
+    there, so the names are never referenced); the tools build keeps them."""
+    from conftest import TOOLS_ONLY_ENV
+    blob = open(spmv_hw.lib_path(dtype), "rb").read()
+    assert not [k for k in TOOLS_ONLY_ENV if k.encode() + b"\0" in blob]
+    tools = spmv_hw.lib_path(dtype, ablations=True)
+    if os.path.exists(tools):
+        tblob = open(tools, "rb").read()
+        assert all(k.encode() + b"\0" in tblob for k in TOOLS_ONLY_ENV)

@@ -1,0 +1,69 @@
+"""bench.py --gpus N without a launcher: the parent starts N ranks itself
+before any GPU call, with the environment torch.distributed.run would give them, relays rank 0's
+JSON line and exits with the workers' worst status. --dry-launch makes every rank print its launch
+environment and exit before touching the GPU, so the plumbing runs here on the CPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(*extra, env=None, timeout=120):
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH, *extra], capture_output=True, text=True, timeout=timeout, env=e)
+
+
+def _lines(text):
+    return [json.loads(ln) for ln in text.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_self_launch_gives_every_rank_its_environment(n):
+    p = _run("--gpus", str(n), "--dry-launch")
+    assert p.returncode == 0, p.stderr
+    out = _lines(p.stdout)
+    assert len(out) == 1 and out[0]["RANK"] == "0"  # only rank 0's line on stdout
+    ranks = out + _lines(p.stderr)
+    assert sorted(int(r["RANK"]) for r in ranks) == list(range(n))
+    for r in ranks:
+        assert r["LOCAL_RANK"] == r["RANK"] and r["WORLD_SIZE"] == str(n) and r["LOCAL_WORLD_SIZE"] == str(n)
+        assert r["MASTER_ADDR"] == "127.0.0.1" and r["MASTER_PORT"] == ranks[0]["MASTER_PORT"]
+        assert r["SPMV_BENCH_LAUNCHER"] == "bench.py" and r["gpus"] == n
+    assert len({r["pid"] for r in ranks}) == n  # one process per rank
+
+
+@pytest.mark.parametrize("codes,want", [("2:3", 3), ("1:7,2:3", 7), ("1:-9", 137), ("0:4", 4)])
+def test_self_launch_exits_with_the_worst_status(codes, want):
+    p = _run("--gpus", "3", "--dry-launch", "--dry-launch-rc", codes)
+    assert p.returncode == want, (p.returncode, p.stderr)
+
+
+def test_self_launch_stops_a_hung_rank_after_another_failed():
+    """A rank that fails leaves the others possibly waiting in a collective: after --spawn-grace
+    seconds the parent kills them (status 128 + 9)."""
+    p = _run("--gpus", "3", "--dry-launch", "--dry-launch-rc", "1:hang,2:5", "--spawn-grace", "1", timeout=60)
+    assert p.returncode == 137, (p.returncode, p.stderr)
+
+
+def test_under_a_launcher_no_second_spawn():
+    """With WORLD_SIZE set (torch.distributed.run), bench.py is one rank and starts nothing."""
+    p = _run("--gpus", "2", "--dry-launch",
+             env={"RANK": "1", "LOCAL_RANK": "1", "WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29999"})
+    assert p.returncode == 0, p.stderr
+    (line,) = _lines(p.stdout)
+    assert line["RANK"] == "1" and line["SPMV_BENCH_LAUNCHER"] is None
+
+
+def test_one_gpu_runs_in_process():
+    p = _run("--dry-launch")
+    assert p.returncode == 0, p.stderr
+    (line,) = _lines(p.stdout)
+    assert line["gpus"] == 1 and line["WORLD_SIZE"] is None

@@ -12,6 +12,7 @@ import pytest
 
 import oracle
 import spmv_hw
+from conftest import TOOLS_ONLY_ENV, tools_env
 from test_gpu_parity import KERNEL_ID, _bitwise, check, run_device
 
 pytestmark = pytest.mark.gpu
@@ -93,7 +94,10 @@ def test_fuzz(torch, monkeypatch, seed, kern, dtype):
     row_ptr, col, val, x, m, unsorted = fuzz_case(seed, dtype)
     monkeypatch.setenv("SPMV_HW_KERNEL", kern.split("_")[0])
     for k, v in ENV.get(kern, {}).items():
-        monkeypatch.setenv(k, v)
+        if k in TOOLS_ONLY_ENV:
+            tools_env(monkeypatch, k, v)
+        else:
+            monkeypatch.setenv(k, v)
     rng = np.random.default_rng(seed)
     vf, block = int(rng.choice([1, 2, 4, 8])), int(rng.choice([1, 7, 97, 700, 4096, 32768, 65536]))
     block = max(block, -(-m // 4096))  # kernel 4: at most one fp64 row chunk (4096) of blocks

@@ -178,16 +178,19 @@ def test_mgpu_set_x_device_waits_for_the_producer(form):
 @pytest.mark.parametrize("steps", [1, 4, 5])
 def test_mgpu_run_pipelined(exchange, steps):
     """spmv_mgpu_run_pipelined: `steps` SpMVs whose exchanges overlap the next SpMV's kernels
-    (double-buffered y; an even step count leaves the result in the second buffer, which then
-    becomes rank 0's y). The result equals the oracle and a plain run afterwards still works."""
+    (double-buffered y; an even step count leaves the result in the second buffer, which is then
+    copied into rank 0's y: its device address does not change). The result equals the oracle and
+    a plain run afterwards still works."""
     lib = spmv_hw.load(np.float64)
     n, z = 300_000, 4_800_000
     rp, col, val, x = _powerlaw_host(lib, n, z)
     mg = spmv_hw.MultiGpu(lib, lib.make_csr_matrix(rp, col, val, n), ndev=_ndev())
     mg.set_x(x)
     ref = oracle.spmv_gold(rp, col, val, x)
+    p0 = mg.y_device_ptr(exchange)
     ms = mg.run_pipelined(exchange, steps)
     assert ms > 0
+    assert mg.y_device_ptr(exchange) == p0
     assert oracle.scaled_error(rp, col, val, x, ref, mg.y(exchange)) <= 1e-12
     mg.run(exchange)
     assert oracle.scaled_error(rp, col, val, x, ref, mg.y(exchange)) <= 1e-12
@@ -230,5 +233,51 @@ def test_mgpu_run_graph(iters):
         assert oracle.scaled_error(r, c, h[2], prev, ref, got) <= 1e-12
         xs = got
     torch.cuda.synchronize()
+    mg.destroy()
+    plan.destroy()
+
+
+@pytest.mark.parametrize("exchange", [spmv_hw.MGPU_GATHER, spmv_hw.MGPU_REDUCE])
+def test_mgpu_graph_after_pipelined_sees_new_x(exchange):
+    """a graph captured before an even-step pipelined run must still write the y that
+    spmv_mgpu_get_y / _y_device read. graph(x1) -> pipelined(2 steps) -> x2 -> graph (replayed,
+    same x buffer): y = A x2, at the address y_device gave before."""
+    import torch
+    lib = spmv_hw.load(np.float64)
+    n, z = 200_000, 3_200_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x1 = spmv_hw.gen_vector(lib, n, seed=6)
+    x2 = spmv_hw.gen_vector(lib, n, seed=7, lo=-1.0)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    mg = spmv_hw.MultiGpu.rank(lib, 0, 1, spmv_hw.mgpu_unique_id(lib), 0, [0, n], n, plan)
+    h = [t.cpu().numpy() for t in (rp, col, val, x1, x2)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    mg.set_x_device(x1)
+    p0 = mg.y_device_ptr(exchange)
+    mg.run_graph(exchange, 2)
+    mg.run_pipelined(exchange, 2)
+    mg.set_x_device(x2)
+    mg.run_graph(exchange, 2)
+    assert mg.y_device_ptr(exchange) == p0
+    ref2 = oracle.spmv_gold(r, c, h[2], h[4])
+    assert oracle.scaled_error(r, c, h[2], h[4], ref2, mg.y(exchange)) <= 1e-12
+    torch.cuda.synchronize()
+    mg.destroy()
+    plan.destroy()
+
+
+def test_mgpu_set_x_device_rejects_x_on_another_device():
+    """the producer event is recorded on rank 0's device, so x must live there."""
+    import torch
+    if _ndev() < 2:
+        pytest.skip("needs a second GPU")
+    lib = spmv_hw.load(np.float64)
+    n = 10_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 160_000, seed=4)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    mg = spmv_hw.MultiGpu.rank(lib, 0, 1, spmv_hw.mgpu_unique_id(lib), 0, [0, n], n, plan)
+    x = torch.ones(n, dtype=torch.float64, device="cuda:1")
+    with pytest.raises(ValueError, match="rank 0 of this handle"):
+        mg.set_x_device(x)
     mg.destroy()
     plan.destroy()

@@ -13,7 +13,7 @@ import pytest
 
 import oracle
 import spmv_hw
-from conftest import DTYPES, FIXTURES, GOLDEN, golden_arrays, manifest
+from conftest import DTYPES, FIXTURES, GOLDEN, golden_arrays, manifest, tools_env
 
 pytestmark = pytest.mark.gpu
 
@@ -48,19 +48,19 @@ def kernel(request, monkeypatch):
     forced (SPMV_BIN_DELTA=1 / 0)."""
     monkeypatch.setenv("SPMV_HW_KERNEL", request.param.split("_")[0])
     if request.param == "tiles_wide":
-        monkeypatch.setenv("SPMV_TILE_NARROW", "0")
+        tools_env(monkeypatch, "SPMV_TILE_NARROW", "0")
     if request.param == "sweep_unpacked":
-        monkeypatch.setenv("SPMV_SWEEP_PACKED", "0")
+        tools_env(monkeypatch, "SPMV_SWEEP_PACKED", "0")
     if request.param == "sweep_rc":  # packed 12-byte words without the delta-coded columns
         monkeypatch.setenv("SPMV_SWEEP_DELTA", "0")
     if request.param == "sweep_det":  # deterministic sweep: LDS adds in a fixed (iteration, wave) order
         monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
     if request.param == "slices_wide":
-        monkeypatch.setenv("SPMV_SLICE_NARROW", "0")
+        tools_env(monkeypatch, "SPMV_SLICE_NARROW", "0")
     if request.param == "binned_delta":  # row-sorted segments with 1-byte deltas, escapes and all
-        monkeypatch.setenv("SPMV_BIN_DELTA", "1")
+        tools_env(monkeypatch, "SPMV_BIN_DELTA", "1")
     if request.param == "binned_u16":  # u16 row offsets
-        monkeypatch.setenv("SPMV_BIN_DELTA", "0")
+        tools_env(monkeypatch, "SPMV_BIN_DELTA", "0")
     return request.param
 
 
@@ -441,13 +441,13 @@ def test_narrow_tiles_bitwise_equal_to_wide(torch, monkeypatch, dtype):
     """8- and 16-bit per-tile column offsets change the bytes streamed, not the arithmetic: all
     three tile representations give bitwise identical y."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=True)
     n = 300_000
     rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
     x = spmv_hw.gen_vector(lib, n, seed=3)
     ys, fmts, nbytes = [], [], []
     for narrow in ("", "16", "0"):
-        monkeypatch.setenv("SPMV_TILE_NARROW", narrow)
+        tools_env(monkeypatch, "SPMV_TILE_NARROW", narrow)
         plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
         y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
         plan.run(x, y)
@@ -471,7 +471,7 @@ def test_narrow_tiles_span_limit(torch, monkeypatch, span, narrow):
     < 65536 -> 16-bit, else 32-bit columns."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
     monkeypatch.delenv("SPMV_TILE_NARROW", raising=False)
-    monkeypatch.setenv("SPMV_TILE_CLUSTER", "0")  # the plain narrow limits (clusters: below)
+    tools_env(monkeypatch, "SPMV_TILE_CLUSTER", "0")  # the plain narrow limits (clusters: below)
     lib = spmv_hw.load(np.float64)
     m = 70_000
     rng = np.random.default_rng(5)
@@ -496,7 +496,7 @@ UNPACKED_VARIANTS = [0, 1, 3, 7, 15, 20, 22]
 def test_sweep_variants_agree(torch, monkeypatch, packed, dtype):
     """Every sweep variant (barrier / loose-sync forms, group counts) computes the same y."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
-    monkeypatch.setenv("SPMV_SWEEP_PACKED", "1" if packed else "0")
+    tools_env(monkeypatch, "SPMV_SWEEP_PACKED", "1" if packed else "0")
     lib = spmv_hw.load(dtype)
     n, z = 200_000, 3_200_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
@@ -521,7 +521,7 @@ def test_sweep_falls_back_to_unpacked_entries_on_sparse_panels(torch, monkeypatc
     per panel over 10M columns: a chunk spans ~80K columns) keeps the 14-byte entries."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     monkeypatch.delenv("SPMV_SWEEP_PACKED", raising=False)
-    monkeypatch.setenv("SPMV_SWEEP_SPLIT", "0")  # 256 small panels, not 13 full ones in pieces
+    tools_env(monkeypatch, "SPMV_SWEEP_SPLIT", "0")  # 256 small panels, not 13 full ones in pieces
     lib = spmv_hw.load(np.float64)
     n, m = 256_000, 10_000_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, 16 * n, seed=4)
@@ -542,12 +542,12 @@ def test_sweep_split_pieces_match_oracle(torch, monkeypatch, dtype):
     """A strong-scaling-like slice (few rows, wide x): full-size panels cut into column pieces
     whose fp64 partial sums k_sweep_combine adds per row; also the same plan forced unsplit."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=True)
     n_full, z_full = 10_000_000, 160_000_000
     r0, r1 = 0, 1_250_000  # rank 0 of 8 (row slice of the 10M/160M matrix, rows only)
     ys = {}
     for split in ("1", "0"):
-        monkeypatch.setenv("SPMV_SWEEP_SPLIT", split)
+        tools_env(monkeypatch, "SPMV_SWEEP_SPLIT", split)
         rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n_full, n_full, z_full, seed=4, row_begin=r0, row_end=r1)
         x = spmv_hw.gen_vector(lib, n_full, seed=6)
         plan = spmv_hw.Plan.from_device(lib, rp, col, val, n_full)
@@ -574,16 +574,16 @@ def test_sweep_fused_combine_bitwise_equals_combine_kernel(torch, monkeypatch):
     panel (two rounds of workgroups, SPMV_SWEEP_PIECES=8); and y matches the oracle."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     monkeypatch.setenv("SPMV_SWEEP_DETERMINISTIC", "1")
-    lib = spmv_hw.load(np.float64)
+    lib = spmv_hw.load(np.float64, ablations=True)
     n_full, z_full = 10_000_000, 160_000_000
     r0, r1 = 1_250_000, 2_500_000  # rank 1 of 8
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n_full, n_full, z_full, seed=4, row_begin=r0, row_end=r1)
     x = spmv_hw.gen_vector(lib, n_full, seed=6)
     ys = {}
     for combine, pieces in (("fused", ""), ("kernel", ""), ("fused", "8"), ("kernel", "8")):
-        monkeypatch.setenv("SPMV_SWEEP_COMBINE", combine)
+        tools_env(monkeypatch, "SPMV_SWEEP_COMBINE", combine)
         if pieces:
-            monkeypatch.setenv("SPMV_SWEEP_PIECES", pieces)
+            tools_env(monkeypatch, "SPMV_SWEEP_PIECES", pieces)
         else:
             monkeypatch.delenv("SPMV_SWEEP_PIECES", raising=False)
         plan = spmv_hw.Plan.from_device(lib, rp, col, val, n_full)
@@ -609,10 +609,10 @@ def test_sweep_fused_combine_bitwise_equals_combine_kernel(torch, monkeypatch):
         check(row_ptr, c, v, xx, ref, y, np.float64)
     # the default (non-deterministic) sweep with the fused combine, 4 and 8 pieces
     monkeypatch.delenv("SPMV_SWEEP_DETERMINISTIC")
-    monkeypatch.setenv("SPMV_SWEEP_COMBINE", "fused")
+    tools_env(monkeypatch, "SPMV_SWEEP_COMBINE", "fused")
     for pieces in ("", "8"):
         if pieces:
-            monkeypatch.setenv("SPMV_SWEEP_PIECES", pieces)
+            tools_env(monkeypatch, "SPMV_SWEEP_PIECES", pieces)
         else:
             monkeypatch.delenv("SPMV_SWEEP_PIECES", raising=False)
         plan = spmv_hw.Plan.from_device(lib, rp, col, val, n_full)
@@ -877,10 +877,10 @@ def test_clustered_tile_columns(torch, monkeypatch, dtype, gaps, clustered):
     m = int(col.max()) + 1
     val = rng.uniform(-1, 1, len(col)).astype(dtype)
     x = rng.uniform(0, 1, m).astype(dtype)
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=True)
     outs = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("SPMV_TILE_CLUSTER", mode)
+        tools_env(monkeypatch, "SPMV_TILE_CLUSTER", mode)
         y, st = run_device(torch, lib, row_ptr, col, val, x, m, expect_kernel="tiles")
         outs[mode] = (y, st["format"])
     assert bool(outs["1"][1] & 16) == clustered and not outs["0"][1] & 16
@@ -1001,12 +1001,12 @@ def test_slices_stencil_narrow_equals_wide(torch, monkeypatch, dtype, points):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     from ab_variants import stencil
     rp, col, val, n = stencil(40 ** 3, points, dtype)
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=True)
     x = spmv_hw.gen_vector(lib, n, seed=3)
     ys = []
     for narrow in ("1", "0"):
         monkeypatch.setenv("SPMV_HW_KERNEL", "slices")
-        monkeypatch.setenv("SPMV_SLICE_NARROW", narrow)
+        tools_env(monkeypatch, "SPMV_SLICE_NARROW", narrow)
         plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
         st = plan.stats()
         assert st["kernel"] == 5 and bool(st["format"] & 1) == (narrow == "1")
@@ -1038,11 +1038,11 @@ def test_slices_clustered_offsets(torch, monkeypatch, dtype):
         rng = np.random.default_rng(5)
         val = rng.uniform(-1, 1, 2 * n).astype(dtype)
         x = rng.uniform(0, 1, m).astype(dtype)
-        lib = spmv_hw.load(dtype)
+        lib = spmv_hw.load(dtype, ablations=True)
         ys = []
         for narrow in ("1", "0"):
             monkeypatch.setenv("SPMV_HW_KERNEL", "slices")
-            monkeypatch.setenv("SPMV_SLICE_NARROW", narrow)
+            tools_env(monkeypatch, "SPMV_SLICE_NARROW", narrow)
             y, st = run_device(torch, lib, row_ptr, cols, val, x, m, expect_kernel="slices")
             assert bool(st["format"] & 16) == (narrow == "1" and clustered)
             ys.append(y)
@@ -1179,9 +1179,9 @@ def test_sweep_workgroup_and_accumulator_settings(torch, monkeypatch, dtype, set
         pytest.skip("SPMV_SWEEP_ACC=32 applies to fp32 matrices only")
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     if setting.startswith("threads"):
-        monkeypatch.setenv("SPMV_SWEEP_THREADS", setting[7:])
+        tools_env(monkeypatch, "SPMV_SWEEP_THREADS", setting[7:])
     else:
-        monkeypatch.setenv("SPMV_SWEEP_ACC", "32")
+        tools_env(monkeypatch, "SPMV_SWEEP_ACC", "32")
     lib = spmv_hw.load(dtype)
     n, m, z = 600_000, 3_000_000, 9_600_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, z, seed=12)
@@ -1215,16 +1215,16 @@ def test_measurement_layout_switches(torch, monkeypatch, dtype, knob):
     """Two layout switches kept for measurements: SPMV_TILE_XCD=1 (the tiles
     dealt XCD-contiguously) on a banded matrix, and SPMV_SWEEP_LANE_ORDER=0 (packed sweep chunks in
     plain column order, hence no delta-coded columns) on a power-law one. y matches the oracle."""
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=True)
     if knob == "tile_xcd":
         monkeypatch.setenv("SPMV_HW_KERNEL", "tiles")
-        monkeypatch.setenv("SPMV_TILE_XCD", "1")
+        tools_env(monkeypatch, "SPMV_TILE_XCD", "1")
         n = 1_000_000
         rp, col, val = spmv_hw.gen_banded(lib, n, 16, seed=2)
         m = n
     else:
         monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
-        monkeypatch.setenv("SPMV_SWEEP_LANE_ORDER", "0")
+        tools_env(monkeypatch, "SPMV_SWEEP_LANE_ORDER", "0")
         n, m = 2_000_000, 10_000_000
         rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, m, 16 * n, seed=13)
     x = spmv_hw.gen_vector(lib, m, seed=6)
@@ -1291,7 +1291,7 @@ def test_binned_xcc_bias_windows(torch, monkeypatch, bias, dtype, m, aligned):
     window (one round of 256 windows in fp32, two rounds in fp64 where W is LDS-capped), a
     partial last pair, a negative and a large bias; x aligned and one element in."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "binned")
-    monkeypatch.setenv("SPMV_BIN_XCC_BIAS", bias)
+    tools_env(monkeypatch, "SPMV_BIN_XCC_BIAS", bias)
     rng = np.random.default_rng(31)
     n = 3000
     row_ptr, col, val, x = random_csr(rng, n, m, rng.integers(0, 30, n), dtype)

@@ -1,10 +1,14 @@
-"""spmv_hw (the reference's entry, csr_hw_wrapper.cpp:193-288) with the RCCL merge: when the units
-sit on distinct GPUs, the slices meet on GPU 0 over xGMI -- an RCCL gather of the disjoint slices
-(default) or, with SPMV_HW_MERGE=reduce, the literal ncclReduce(sum) of full-length partials
-(accum_results' `+=`, csr_hw.cpp:1531-1565) -- and one D2H copy brings y home. The box has one
-GPU, so these tests run the RCCL branch with one unit (forced by SPMV_HW_MERGE; a one-rank
-reduce still goes through RCCL); the driver's 8-GPU node takes the same code with 8. y is checked
-against the oracle's spmv_gold (csr.cpp:184-194) and the golden fixtures."""
+"""spmv_hw (the reference's entry, csr_hw_wrapper.cpp:193-288) with the RCCL merge: with
+SPMV_HW_MERGE=gather (or reduce) and the units on distinct GPUs, the slices meet on GPU 0 over
+xGMI -- an RCCL gather of the disjoint slices, or the literal ncclReduce(sum) of full-length
+partials (accum_results' `+=`, csr_hw.cpp:1531-1565) -- and one D2H copy brings y home. The
+default (auto) is the per-GPU PCIe merge. The box has one GPU, so these tests run the RCCL branch
+with one unit: there a gather issues NO RCCL call (its schedule has no exchange op; the trace
+says "0 RCCL calls") and only the reduce goes through RCCL (one ncclReduce that copies the
+partial). The multi-rank send / receive arithmetic of the same schedule is executed on the CPU by
+tests/test_exchange_schedule.py (gloo replay). y is checked against the oracle's spmv_gold
+(csr.cpp:184-194) and the golden fixtures."""
+import re
 import os
 import subprocess
 import sys
@@ -14,7 +18,7 @@ import pytest
 
 import oracle
 import spmv_hw
-from conftest import DTYPES, FIXTURES, GOLDEN, golden_arrays, manifest
+from conftest import DTYPES, FIXTURES, GOLDEN, golden_arrays, manifest, tools_env
 
 pytestmark = pytest.mark.gpu
 
@@ -65,6 +69,15 @@ def test_rccl_merge_on_golden_fixtures(monkeypatch, capfd, merge, name, dtype, t
     assert out.count("Result accumulation time : ") == 2
     assert out.count("Total time  : ") == 2
     assert "RCCL merge" in err  # the trace names the branch that ran
+    calls = [int(c) for c in re.findall(r"(\d+) RCCL calls", err)]
+    assert len(calls) == 2
+    ndev = _ndev()
+    if merge == "reduce":  # one ncclReduce per rank, also at one rank
+        assert calls == [ndev, ndev]
+    else:  # rank 0 receives every other non-empty slice, every other rank sends its own
+        assert all(c <= 2 * (ndev - 1) for c in calls)
+        if ndev == 1:
+            assert calls == [0, 0]
 
 
 @pytest.mark.parametrize("pipeline", ["1", "0"])
@@ -108,10 +121,11 @@ def test_rccl_merge_refuses_shared_gpus():
     assert "needs one unit per GPU" in p.stderr
 
 
-def test_auto_merge_keeps_host_for_shared_gpus(monkeypatch, capfd):
-    """Automatic choice: 3 virtual units on the box's one GPU cannot form an RCCL clique, so the
-    per-unit PCIe merge runs (and gives the oracle's y)."""
-    monkeypatch.setenv("SPMV_NGPUS", str(_ndev() + 2))
+@pytest.mark.parametrize("extra", [0, 2])
+def test_auto_merge_is_host(monkeypatch, capfd, extra):
+    """Automatic choice: the per-unit PCIe merge (y_fpga is host memory), with one
+    unit per GPU and with virtual units sharing a GPU; y is the oracle's."""
+    monkeypatch.setenv("SPMV_NGPUS", str(_ndev() + extra))
     monkeypatch.delenv("SPMV_HW_MERGE", raising=False)
     monkeypatch.setenv("SPMV_HW_TRACE", "1")
     lib = spmv_hw.load(np.float64)
@@ -131,7 +145,7 @@ def test_host_merge_pieces_of_several_units(monkeypatch, split):
     whole pieces (split 0); y matches the oracle and a second call adds A*x once more."""
     monkeypatch.setenv("SPMV_NGPUS", str(_ndev() + 2))
     monkeypatch.setenv("SPMV_HW_MERGE", "host")
-    monkeypatch.setenv("SPMV_HW_ADD_SPLIT", split)
+    tools_env(monkeypatch, "SPMV_HW_ADD_SPLIT", split)
     lib = spmv_hw.load(np.float64)
     n, z = 1_000_000, 16_000_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=9)

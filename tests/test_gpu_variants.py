@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import spmv_hw
+from conftest import tools_env
 
 pytestmark = pytest.mark.gpu
 
@@ -175,7 +176,7 @@ def test_binned_segment_offsets_past_2_31(monkeypatch, dtype, variant, delta):
     addresses), so half the segments lie past the boundary; y must match the oracle."""
     import torch
     import oracle
-    monkeypatch.setenv("SPMV_BIN_DELTA", delta)
+    tools_env(monkeypatch, "SPMV_BIN_DELTA", delta)
     lib, plan, x = _plan(monkeypatch, "binned", dtype, n=200_000, z=3_200_000)
     st = plan.stats()
     assert st["kernel"] == 6 and bool(st["format"] & 32) == (delta == "1")
