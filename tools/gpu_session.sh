@@ -13,8 +13,11 @@ fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
 run() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
   echo "== $name: $*" | tee -a "$OUT/session.log"
+  # heartbeat: a step that prints nothing for minutes (a bench before its one line) still shows life
+  ( while sleep 30; do date +%T >> "$OUT/heartbeat"; done ) & local hb=$!
   timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
+  kill $hb 2>/dev/null; wait $hb 2>/dev/null
   echo "== $name rc=$rc" | tee -a "$OUT/session.log"
   tail -5 "$OUT/$name.log"
   if fatal $rc; then echo "FATAL step $name rc=$rc; stopping" | tee -a "$OUT/session.log"; exit $rc; fi
@@ -23,6 +26,9 @@ run() {  # name seconds cmd...
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    tests_sel) run pytest_sel 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    selflaunch) SPMV_BENCH_BACKEND=gloo run selflaunch_strong 600 python bench.py --gpus 2 --steps 5 --warmup 2 ;;
+    selflaunch_weak) SPMV_BENCH_BACKEND=gloo run selflaunch_weak 600 python bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak ;;
     tests_all) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
