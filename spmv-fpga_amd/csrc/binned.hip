@@ -114,13 +114,17 @@ __device__ unsigned long long g_abl_bin[2][4 * 4096];
 
 // Pass 1: unit u = entries [ub[u], ub[u+1]) of window uwin[u] (both multiples of PER).
 // AL: x is 16-byte aligned, so the window is staged with 16-byte loads.
+// mirror != 0 (variant 7, same y): the 16-byte product vector of entries [i, i + PER) is stored at
+// mirror - i instead of i (mirror = the last vector's index), so the product stores run down the
+// array while the entry loads run up it, and the two streams keep no fixed address distance
+// (config 5's per-plan modes). Pass 2 reads them back at the same place.
 // POL (variants 3-5, the same y): bit 0 = temporal (default-policy) product stores instead of
 // non-temporal ones, bit 1 = temporal entry loads
 template <typename V, bool AL, int POL = 0>
 __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint32_t ncols, uint32_t W0, uint32_t W1,
                                                    const uint64_t *__restrict__ ub, const uint32_t *__restrict__ uwin,
                                                    const uint16_t *__restrict__ colw, const V *__restrict__ val,
-                                                   V *__restrict__ prod)
+                                                   V *__restrict__ prod, uint64_t mirror)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     V *xs = reinterpret_cast<V *>(smem);
@@ -198,10 +202,11 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
                     const V xq = xs[cq == kBinSent ? 0 : cq];
                     pr[q] = cq == kBinSent ? V(0) : v[k][q] * xq;
                 }
+                const uint64_t o = mirror ? mirror - i : i;
                 if constexpr (POL & 1)
-                    *reinterpret_cast<VT *>(prod + i) = pr;
+                    *reinterpret_cast<VT *>(prod + o) = pr;
                 else
-                    __builtin_nontemporal_store(pr, reinterpret_cast<VT *>(prod + i));
+                    __builtin_nontemporal_store(pr, reinterpret_cast<VT *>(prod + o));
             }
         }
     }
@@ -223,7 +228,7 @@ template <typename V, bool DELTA, int ABL = 0>
 __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, const void *__restrict__ rowp,
                                                    const uint64_t *__restrict__ seg,
                                                    const uint32_t *__restrict__ panel_row, uint32_t nwin,
-                                                   uint32_t npan, uint32_t slots, V *__restrict__ y)
+                                                   uint32_t npan, uint32_t slots, V *__restrict__ y, uint64_t mirror)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double *ys = reinterpret_cast<double *>(smem);
@@ -299,7 +304,7 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
                 uint64_t ld = at[k];
                 if constexpr (ABL == 2)
                     ld = (ld & ~(uint64_t)(16 * STEP - 1)) == 0 ? ld : (ld & (16 * STEP - 1));
-                v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + ld));
+                v[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(prod + (mirror ? mirror - ld : ld)));
                 if (DELTA)
                     dl[k] = __builtin_nontemporal_load(reinterpret_cast<const DT *>(rows8 + ld));
                 else
@@ -493,6 +498,9 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
 {
     if (p.nr_rows == 0)
         return hipSuccess;
+    constexpr uint64_t PERV = 16 / sizeof(ValueType);
+    // variant 7: mirrored products (k_bin_mul); the index of the last product vector
+    const uint64_t mirror = p.variant == 7 ? std::max<uint64_t>(p.ent_pad, PERV) - PERV : 0;
     if (p.b_nunits) {
         const size_t lds1 = size_t(std::max(p.b_W, p.b_W1)) * sizeof(ValueType);
         const bool al = (reinterpret_cast<uintptr_t>(d_x) & 15u) == 0;
@@ -506,15 +514,15 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
         if (pol && al) {
 #define BINPOL(P)                                                                                          \
     launch_or_warm(warm, k_bin_mul<ValueType, true, P>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x, \
-                   (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod)
+                   (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod, mirror)
             if (pol == 1) BINPOL(1); else if (pol == 2) BINPOL(2); else BINPOL(3);
 #undef BINPOL
         } else if (al || warm)
             launch_or_warm(warm, k_bin_mul<ValueType, true>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x,
-                           (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
+                           (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod, mirror);
         if (!al || warm)
             launch_or_warm(warm, k_bin_mul<ValueType, false>, dim3((unsigned)p.b_nunits), dim3(kBinT), lds1, s, d_x,
-                           (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod);
+                           (uint32_t)p.nr_cols, p.b_W, p.b_W1, p.d_b_ub, p.d_b_uwin, p.d_b_colw, p.d_b_val, p.d_b_prod, mirror);
     }
     const size_t lds2 = (size_t(p.panel_rmax) + 1) * sizeof(double);
     // variants 1 / 2 (tests): segment offsets rebased past 2^31 / 2^32, the product and row arrays
@@ -526,23 +534,25 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
         reinterpret_cast<uintptr_t>(p.d_b_prod) - base * sizeof(ValueType));
     const void *rowp = reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(p.d_b_rowp) -
                                                       base * (p.b_delta ? 1 : 2));
+    // pass 2 sees offsets ld + base against prod - base: the mirrored index is mirror + 2 base - ld
+    const uint64_t mirror2 = mirror ? mirror + 2 * base : 0;
 #ifdef SPMV_ABLATIONS
     if (p.b_delta && (p.variant == 51 || p.variant == 52)) {
         if (p.variant == 51)
             launch_or_warm(warm, k_bin_acc<ValueType, true, 1>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod,
-                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
+                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
         else
             launch_or_warm(warm, k_bin_acc<ValueType, true, 2>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod,
-                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
+                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
         return hipGetLastError();
     }
 #endif
     if (p.b_delta)
         launch_or_warm(warm, k_bin_acc<ValueType, true>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod, rowp,
-                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
+                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
     else
         launch_or_warm(warm, k_bin_acc<ValueType, false>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod, rowp,
-                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y);
+                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
     return hipGetLastError();
 }
 

@@ -903,10 +903,11 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
         // 2^32 entries (prod and rowp rebased the other way: the same addresses), which drives the
         // 64-bit bound widening after readlane (binned.hip, k_bin_acc) without a 2^31-entry matrix
         // 3-6 (same y): pass-1 cache policy (3: temporal product stores, 4: temporal entry
-        // loads, 5: both, 6: non-temporal stores; 0 = the plan's choice); 51 / 52 (tools
+        // loads, 5: both, 6: non-temporal stores; 0 = the plan's choice); 7 (same y): mirrored
+        // products (stored down the array while the entries stream up it); 51 / 52 (tools
         // library): pass-2 ablations, binned.hip
-        if (variant > 6 && !(variant >= 51 && variant <= 52)) {
-            set_error("spmv_plan_set_variant: binned variants are 0-6");
+        if (variant > 7 && !(variant >= 51 && variant <= 52)) {
+            set_error("spmv_plan_set_variant: binned variants are 0-7");
             return 1;
         }
         if (p->d_b_seg_hi) {

@@ -192,16 +192,18 @@ def test_binned_segment_offsets_past_2_31(monkeypatch, dtype, variant, delta):
     err = oracle.scaled_error(r, c, h[2], h[3], ref, y.cpu().numpy())
     assert err <= (1e-12 if dtype == np.float64 else 2e-6), err
     with pytest.raises(RuntimeError, match="binned variants"):
-        plan.set_variant(7)
+        plan.set_variant(8)
     plan.set_variant(0)
     plan.destroy()
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 6], ids=["plain_stores", "plain_loads", "plain_both", "nt_stores"])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6, 7], ids=["plain_stores", "plain_loads", "plain_both", "nt_stores",
+                                                          "mirrored"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_binned_pass1_cache_policy_variants(monkeypatch, dtype, variant):
     """Binned variants 3-6 change only pass 1's cache policy (temporal product stores / entry
-    loads / both; 6: non-temporal stores): y matches the oracle as with the default."""
+    loads / both; 6: non-temporal stores), 7 where the products go (mirrored: stored down the
+    array, read back there by pass 2): y matches the oracle as with the default."""
     import torch
     import oracle
     lib, plan, x = _plan(monkeypatch, "binned", dtype, n=200_000, z=3_200_000)

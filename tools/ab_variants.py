@@ -57,6 +57,10 @@ def main():
               or (v.split(":")[0].startswith("blocked") and v.split(":")[1] == "1")
               or (v.split(":")[0].startswith("binned") and int(v.split(":")[1]) in (51, 52))
               for v in a.variants.split(",") if ":" in v)
+    # layout switches of a kernel spec (suffixes below) are read by the tools library only too
+    kerns = {v.split(":")[0].partition("#")[0] for v in a.variants.split(",") if ":" in v}
+    abl = abl or any("@" in k or "^" in k or (k.startswith("binned") and "~" in k)
+                     or k.rstrip("0123456789").endswith(("U", "S", "F", "X", "H", "W", "L", "F32")) for k in kerns)
     if abl:
         os.environ["SPMV_HW_ABLATIONS"] = "1"
     dtype = np.float64 if a.dtype == "f64" else np.float32
@@ -81,7 +85,8 @@ def main():
         for v in variants:
             k, var = v.split(":")
             if k not in plans:  # "sweep@512" = 512-thread workgroups, "sweepU" = unpacked entries
-                kern, _, threads = k.partition("@")
+                kern = k.partition("#")[0]  # "binned#2": a second plan of the same layout (duplicate)
+                kern, _, threads = kern.partition("@")
                 kern, _, pskew = kern.partition("^")  # "binned^4096": SPMV_BIN_PROD_SKEW=4096
                 if pskew:
                     os.environ["SPMV_BIN_PROD_SKEW"] = pskew
@@ -163,6 +168,7 @@ def main():
                 plan.set_timing(False)
                 res[v].append(ms)
         out = {"workload": wl, "dtype": a.dtype, "nnz": st["nr_nzeros"], "alg_bytes": st["algorithmic_bytes"],
+               "library": os.path.basename(os.path.dirname(lib.path)),
                "plans": {k: {kk: p.stats()[kk] for kk in ("kernel", "nr_tiles", "device_bytes")} for k, p in plans.items()}}
         # (device_bytes tells packed 12-B entries from unpacked 14-B ones)
         for v in variants:
