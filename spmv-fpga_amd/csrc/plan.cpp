@@ -646,7 +646,7 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_steal, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, (void *)d_s_row16, (void *)d_s_d8, (void *)d_s_dbase, (void *)d_s_side, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
                       (void *)d_sbase, (void *)d_slice_len, (void *)d_b_val, (void *)d_b_colw, (void *)d_b_rowp,
@@ -873,7 +873,8 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
     st->format = (p->kernel == kKernelSlices && p->slice_off_bytes < 4 ? 1 : 0) | (p->slice_clustered ? 16 : 0) |
                  (p->kernel == kKernelSlices && p->slice_off_bytes == 1 ? 8 : 0) | (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) | (p->sweep_delta ? 64 : 0) |
                  (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0) |
-                 (p->kernel == kKernelBinned && p->b_delta ? 32 : 0);
+                 (p->kernel == kKernelBinned && p->b_delta ? 32 : 0) |
+                 (p->kernel == kKernelSweep && p->sweep_steal && p->sweep_variant != 36 ? 128 : 0);
     return 0;
 }
 
@@ -893,9 +894,9 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
     }
 #endif
     if (p->kernel == kKernelSweep) {
-        // every variant but the default (28) reads the 12-byte rc words, which a delta plan
-        // rebuilds on first use
-        if (variant != 28 && sweep_materialize_rc(*p))
+        // every variant but the default (28) and 36 (the default without work stealing) reads the
+        // 12-byte rc words, which a delta plan rebuilds on first use
+        if (variant != 28 && variant != 36 && sweep_materialize_rc(*p))
             return 1;
         p->sweep_variant = variant;
     } else if (p->kernel == kKernelBinned) {

@@ -196,14 +196,18 @@ __device__ __forceinline__ void write_panel(const A *__restrict__ ylds, uint32_t
 
 // y[r0 + i] = sum over the panel's pieces u (in order) of part[u * stride + i]; panels of one
 // piece were written by the sweep itself
+// steal != null: also re-arms the panel's work-stealing counters for the next launch
 template <typename V, typename A>
 __global__ __launch_bounds__(256) void k_sweep_combine(const uint32_t *__restrict__ panel_row,
                                                        const uint32_t *__restrict__ panel_unit,
                                                        const A *__restrict__ part, uint32_t stride,
-                                                       V *__restrict__ y)
+                                                       V *__restrict__ y, unsigned long long *__restrict__ steal)
 {
     const uint32_t p = blockIdx.y;
     const uint32_t u0 = panel_unit[p], u1 = panel_unit[p + 1];
+    if (steal && blockIdx.x == 0)
+        for (uint32_t t = threadIdx.x; t < u1 - u0; t += 256)
+            steal[u0 + t] = 0;
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (u1 - u0 < 2 || i >= R)
@@ -309,14 +313,77 @@ __device__ unsigned long long g_abl_wg[4 * 4096];
     do {             \
     } while (0)
 #endif
-template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double, bool DL = false>
+// Work stealing among the pieces of a panel (split plans, ST): a unit's workgroup iterations are
+// tasks. Its first kAhead tasks are its own; the rest it claims one at a time from the front of
+// its counter (steal[u], low word), and once those are gone it claims iterations from the back of
+// its sibling pieces (high word of theirs). Siblings share the panel, so a stolen iteration adds
+// into the thief's own LDS rows and partial sums; k_sweep_combine adds every piece's partials as
+// before and re-arms the counters. An owner's front claim of iteration kAhead + f and a thief's
+// back claim of n - 1 - b are granted only while kAhead + f + b < n, read from the same 64-bit
+// word by the same atomic add, so no iteration is taken twice or left out. The siblings' column
+// ranges lie on other XCDs (pieces are dealt round-robin), so a stolen iteration gathers x lines
+// its own L2 does not hold: stealing pays only in the tail.
+struct SweepThief {
+    uint32_t self, u0, pieces, k;  // own unit, first unit of the panel, pieces, siblings tried
+    uint32_t vic, vn;              // unit claimed from (self while front), its iterations
+    uint64_t ve0, ve1;             // its entry range
+    bool front, end;
+};
+
+__device__ __forceinline__ unsigned long long thief_issue(const SweepThief &t, unsigned long long *steal)
+{
+    return __hip_atomic_fetch_add(steal + t.vic, t.front ? 1ull : (1ull << 32), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the claim `old` (the counter before this add) granted: (b, e) = the task's entries
+__device__ __forceinline__ bool thief_take(const SweepThief &t, unsigned long long old, uint32_t qg, uint32_t ahead,
+                                           uint64_t &b, uint64_t &e)
+{
+    const uint32_t f = (uint32_t)old, k = (uint32_t)(old >> 32);
+    if ((uint64_t)ahead + f + k >= t.vn)
+        return false;
+    const uint32_t it = t.front ? ahead + f : t.vn - 1 - k;
+    b = t.ve0 + (uint64_t)it * qg;
+    e = t.ve1;
+    return true;
+}
+
+// the next sibling piece (cyclic after this unit), or the end
+__device__ __forceinline__ void thief_next(SweepThief &t, const uint32_t *__restrict__ unit_ent, uint32_t qg)
+{
+    t.front = false;
+    if (++t.k >= t.pieces) {
+        t.end = true;
+        return;
+    }
+    t.vic = t.u0 + (t.self - t.u0 + t.k) % t.pieces;
+    t.ve0 = unit_ent[t.vic];
+    t.ve1 = unit_ent[t.vic + 1];
+    t.vn = (uint32_t)((t.ve1 - t.ve0 + qg - 1) / qg);
+}
+
+// claims until a task is granted (true) or none is left anywhere (false)
+__device__ bool thief_claim_sync(SweepThief &t, unsigned long long *steal, const uint32_t *__restrict__ unit_ent,
+                                 uint32_t qg, uint32_t ahead, uint64_t &b, uint64_t &e)
+{
+    while (!t.end) {
+        if (thief_take(t, thief_issue(t, steal), qg, ahead, b, e))
+            return true;
+        thief_next(t, unit_ent, qg);
+    }
+    return false;
+}
+
+template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double, bool DL = false,
+          bool ST = false>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
     A *__restrict__ part, uint32_t stride, uint32_t *__restrict__ pcnt, const V *__restrict__ x,
     V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
-    const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side)
+    const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -328,22 +395,72 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
     const uint64_t e0 = unit_ent[blockIdx.x], e1 = unit_ent[blockIdx.x + 1];
     __shared__ uint32_t progress[T / 64];
+    constexpr uint64_t kGroup = 2ull * T;
+    // ST: the ring of tasks (the entry range of one workgroup iteration) that thread 0 fills
+    // kAhead tasks ahead of itself; the loose sync keeps every wave within LAG < kAhead tasks
+    constexpr uint32_t QG = Q * (uint32_t)kGroup, kRing = 8, kAhead = 3;
+    static_assert(!ST || (LAG > 0 && LAG < (int)kAhead && kAhead + LAG + 1 <= kRing), "steal ring sizing");
+    __shared__ uint32_t ring_b[ST ? kRing : 1], ring_e[ST ? kRing : 1], ring_s[ST ? kRing : 1];
+    SweepThief th{blockIdx.x, 0, pieces, 0, blockIdx.x, 0, e0, e1, true, true};
     ABL_WG_STAMP(0);
     ABL_WG_IDS();
     for (uint32_t i = threadIdx.x; i <= R; i += T)
         ylds[i] = A(0);
     if (threadIdx.x < T / 64)
         progress[threadIdx.x] = 0;
+    if constexpr (ST) {
+        if (threadIdx.x == 0) {
+            th.u0 = panel_unit[p];
+            th.vn = (uint32_t)((e1 - e0 + QG - 1) / QG);
+            th.end = false;
+            for (uint32_t t = 0; t < kAhead; ++t) {  // the unit's first tasks are its own
+                uint64_t b = 0, e = 0;
+                bool got = t < th.vn;
+                if (got)
+                    b = e0 + (uint64_t)t * QG, e = e1;
+                else
+                    got = thief_claim_sync(th, steal, unit_ent, QG, kAhead, b, e);
+                ring_b[t] = got ? (uint32_t)b : 0xFFFFFFFFu;
+                ring_e[t] = got ? (uint32_t)e : 0u;
+                ring_s[t] = t + 1;
+            }
+        }
+    }
     __syncthreads();
     uint32_t iter = 0;
     A sink = 0;  // ablations 8/9 only
-    constexpr uint64_t kGroup = 2ull * T;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane2 = 2u * (threadIdx.x & 63);
-    // branch-free body: a group past the panel end re-reads the panel's last chunk (valid
-    // memory) and adds into the scratch slot R, so every load of the Q groups issues together
-    const uint64_t last_chunk = e1 > e0 ? e1 - 128 : e0;
-    for (uint64_t base = e0; base < e1; base += Q * kGroup) {
+    uint64_t base = e0, bound = e1;  // this iteration's entries: [base, base + QG) below bound
+    unsigned long long pend = 0;     // ST, thread 0: the claim issued for task s + kAhead
+    bool issued = false;
+    for (uint32_t s = 0;; ++s) {
+        if constexpr (ST) {
+            if (threadIdx.x == 0 && !th.end) {  // its result is consumed after this task's gathers
+                pend = thief_issue(th, steal);
+                issued = true;
+            } else {
+                issued = false;
+            }
+            const uint32_t slot = s % kRing;
+            // written kAhead tasks ago unless thread 0 is in a claim loop (the tail); bounded wait
+            uint32_t spin = 0;
+            while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ring_s[slot], __ATOMIC_ACQUIRE,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP)) != s + 1 &&
+                   ++spin < (1u << 24))
+                __builtin_amdgcn_s_sleep(1);
+            const uint32_t rb = __builtin_amdgcn_readfirstlane(ring_b[slot]);
+            if (rb == 0xFFFFFFFFu || spin >= (1u << 24))
+                break;
+            base = rb;
+            bound = __builtin_amdgcn_readfirstlane(ring_e[slot]);
+        } else {
+            if (base >= e1)
+                break;
+        }
+        // branch-free body: a group past the unit's end re-reads its last chunk (valid memory)
+        // and adds into the scratch slot R, so every load of the Q groups issues together
+        const uint64_t last_chunk = bound > e0 || ST ? bound - 128 : e0;
         u32x2 w[Q];
         uint32_t cb[Q];
         V v[Q][2];
@@ -353,7 +470,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             uint64_t wbase = base + q * kGroup + 128ull * wave;  // this wave's chunk
-            ok[q] = wbase < e1;                                   // wave-uniform
+            ok[q] = wbase < bound;                                // wave-uniform
             wbase = ok[q] ? wbase : last_chunk;
             if constexpr (ABL == 3 || ABL == 4 || ABL == 9)  // ablation: entries re-read from the unit's first 4K (L2-resident)
                 wbase = e0 + ((wbase - e0) & 4095u);
@@ -456,6 +573,25 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
                 pv[2 * q + 1] = A(v[q][1]) * A(xv[q][1]);
             }
             lds_add_n<2 * Q>(ylds, ri, pv);
+        }
+        if constexpr (ST) {
+            if (threadIdx.x == 0) {  // the task kAhead ahead: the claim issued above, or a claim loop
+                uint64_t b = 0, e = 0;
+                bool got = false;
+                if (issued) {
+                    got = thief_take(th, pend, QG, kAhead, b, e);
+                    if (!got) {
+                        thief_next(th, unit_ent, QG);
+                        got = thief_claim_sync(th, steal, unit_ent, QG, kAhead, b, e);
+                    }
+                }
+                const uint32_t slot = (s + kAhead) % kRing;
+                ring_b[slot] = got ? (uint32_t)b : 0xFFFFFFFFu;
+                ring_e[slot] = got ? (uint32_t)e : 0u;
+                __hip_atomic_store(&ring_s[slot], s + kAhead + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else {
+            base += QG;
         }
         if constexpr (LAG == 0) {
             __syncthreads();
@@ -968,12 +1104,13 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #define PKN(NT, Q, LAG, ABL)                                                                        \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
-                       (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr)
+                       (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr, \
+                       (unsigned long long *)nullptr)
     // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
-#define PKD()                                                                                         \
-    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true>, grid, block, lds, s, p.d_s_col, \
+#define PKD(ST)                                                                                       \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
-                       p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side)
+                       p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
@@ -1008,7 +1145,12 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 35: PK(2, 2); break;  // variant 28 on the 12-byte rc words of a delta plan (A/B)
         default:
             if (p.sweep_delta) {
-                PKD();
+                // split plans steal iterations among a panel's pieces; variant 36 = the static split
+                if (p.sweep_steal && p.sweep_variant != 36) {
+                    PKD(true);
+                } else {
+                    PKD(false);
+                }
             } else {
                 PK(2, 2);
             }
@@ -1043,7 +1185,7 @@ static void launch_sweep_a(const spmv_plan &p, const ValueType *d_x, ValueType *
     if (p.sweep_split > 1 && !p.d_panel_cnt) {  // env SPMV_SWEEP_COMBINE=kernel
         const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
         launch_or_warm(warm, k_sweep_combine<ValueType, A>, grid, dim3(256), 0, s, p.d_panel_row, p.d_panel_unit,
-                       reinterpret_cast<const A *>(p.d_part), p.panel_rmax + 1, d_y);
+                       reinterpret_cast<const A *>(p.d_part), p.panel_rmax + 1, d_y, p.d_steal);
     }
 }
 
@@ -1220,6 +1362,9 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     p.nunits = U;
     if (multi) {
         SPMV_TRY(hipMalloc((void **)&p.d_part, (uint64_t)U * (uint64_t(rmax_used) + 1) * acc));
+        // work-stealing counters (zero; every k_sweep_combine re-arms them)
+        SPMV_TRY(hipMalloc((void **)&p.d_steal, (uint64_t)U * 8));
+        SPMV_TRY(hipMemsetAsync(p.d_steal, 0, (uint64_t)U * 8, s));
         // env SPMV_SWEEP_COMBINE=fused: the last piece of each panel combines inside the sweep
         // launch instead of k_sweep_combine. Measured slower on the N = 8 slice of the 10M/160M
         // matrix (0.147 vs 0.128 ms, profiles/r03_ab_sweep_combine.jsonl): the panels of a one-round
@@ -1386,6 +1531,9 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                     (void)hipFree(d_sidx);
                     SW_TRY(e);
                     p.sweep_delta = true;
+                    // split plans run the default kernel with work stealing among a panel's pieces
+                    // (the separate combine kernel re-arms the counters)
+                    p.sweep_steal = p.sweep_split > 1 && p.d_steal && !p.d_panel_cnt;
                     // the default kernel reads only the 11-byte entries: the rc words are freed
                     // (rebuilt by sweep_materialize_rc for a variant that reads them)
                     SW_TRY(hipFree(p.d_s_col));

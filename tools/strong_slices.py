@@ -29,6 +29,10 @@ def main():
     ap.add_argument("--slices", default="ends", help="'all' slices, or first+last only")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tag", default=None, help="recorded as _setting in every line (e.g. the env under test)")
+    ap.add_argument("--variants", default=None,
+                    help="comma list of spmv_plan_set_variant values timed interleaved on each slice's plan "
+                         "(e.g. 28,36: the split sweep with and without work stealing)")
+    ap.add_argument("--rounds", type=int, default=5, help="with --variants: interleaved rounds")
     a = ap.parse_args()
     dtype = np.float64 if a.dtype == "f64" else np.float32
     lib = spmv_hw.load(dtype)
@@ -39,7 +43,7 @@ def main():
     for N in [int(v) for v in a.ns.split(",")]:
         b = lib.partition_rows(rp_full, N)
         ranks = range(N) if a.slices == "all" or N <= 2 else (0, N - 1)
-        worst, per = 0.0, {}
+        worst, per, worst_v = 0.0, {}, {}
         for r in ranks:
             r0, r1 = spmv_dist.row_slice(b, r)
             rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4, row_begin=r0, row_end=r1)
@@ -48,13 +52,33 @@ def main():
             y = torch.empty(r1 - r0, dtype=x.dtype, device="cuda")
             for _ in range(3):
                 plan.run(x, y)
-            plan.set_timing(True)
-            for _ in range(a.reps):
-                plan.run(x, y)
-            ms, _, _ = plan.timing()
             st = plan.stats()
-            per[r] = {"rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "ms": round(ms, 5),
-                      "panels": st["nr_tiles"]}
+            if a.variants:  # interleaved A/B of plan variants on this slice (median per variant)
+                vs = [int(v) for v in a.variants.split(",")]
+                times = {v: [] for v in vs}
+                for _ in range(a.rounds):
+                    for v in vs:
+                        plan.set_variant(v)
+                        plan.run(x, y)
+                        plan.set_timing(True)
+                        for _ in range(a.reps):
+                            plan.run(x, y)
+                        times[v].append(plan.timing()[0])
+                        plan.set_timing(False)
+                med = {v: float(np.median(t)) for v, t in times.items()}
+                per[r] = {"rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "panels": st["nr_tiles"],
+                          "format": st["format"], "variants_ms": {str(v): round(m, 5) for v, m in med.items()},
+                          "variants_min_ms": {str(v): round(min(t), 5) for v, t in times.items()}}
+                ms = med[vs[0]]
+                for v in vs:
+                    worst_v[v] = max(worst_v.get(v, 0.0), med[v])
+            else:
+                plan.set_timing(True)
+                for _ in range(a.reps):
+                    plan.run(x, y)
+                ms, _, _ = plan.timing()
+                per[r] = {"rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "ms": round(ms, 5),
+                          "panels": st["nr_tiles"]}
             worst = max(worst, ms)
             plan.destroy()
             torch.cuda.empty_cache()
@@ -63,7 +87,9 @@ def main():
             base = worst
         print(json.dumps({"n_gpus": N, "dtype": a.dtype, "slowest_slice_ms": round(worst, 5),
                           "aggregate_GFLOPs": round(gflops, 1), "speedup_vs_1": round(base / worst, 3),
-                          "slices": per, **({"_setting": a.tag} if a.tag else {})}), flush=True)
+                          "slices": per, **({"slowest_by_variant_ms": {str(v): round(t, 5) for v, t in worst_v.items()}}
+                                            if worst_v else {}),
+                          **({"_setting": a.tag} if a.tag else {})}), flush=True)
 
 
 if __name__ == "__main__":
