@@ -894,9 +894,10 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
     }
 #endif
     if (p->kernel == kKernelSweep) {
-        // every variant but the default (28) and 36 (the default without work stealing) reads the
-        // 12-byte rc words, which a delta plan rebuilds on first use
-        if (variant != 28 && variant != 36 && sweep_materialize_rc(*p))
+        // every variant but the default (28) and 36-38 (the default with the static split, or with
+        // half / all of each unit's iterations claimable) reads the 12-byte rc words, which a
+        // delta plan rebuilds on first use
+        if ((variant < 36 || variant > 38) && variant != 28 && sweep_materialize_rc(*p))
             return 1;
         p->sweep_variant = variant;
     } else if (p->kernel == kKernelBinned) {

@@ -314,21 +314,30 @@ __device__ unsigned long long g_abl_wg[4 * 4096];
     } while (0)
 #endif
 // Work stealing among the pieces of a panel (split plans, ST): a unit's workgroup iterations are
-// tasks. Its first kAhead tasks are its own; the rest it claims one at a time from the front of
-// its counter (steal[u], low word), and once those are gone it claims iterations from the back of
-// its sibling pieces (high word of theirs). Siblings share the panel, so a stolen iteration adds
-// into the thief's own LDS rows and partial sums; k_sweep_combine adds every piece's partials as
-// before and re-arms the counters. An owner's front claim of iteration kAhead + f and a thief's
-// back claim of n - 1 - b are granted only while kAhead + f + b < n, read from the same 64-bit
-// word by the same atomic add, so no iteration is taken twice or left out. The siblings' column
-// ranges lie on other XCDs (pieces are dealt round-robin), so a stolen iteration gathers x lines
-// its own L2 does not hold: stealing pays only in the tail.
+// tasks. Its first S = static_iters(n) tasks are its own (all but the last tail16/16 of them, at
+// least kAhead); the rest it claims one at a time from the front of its counter (steal[u], low
+// word), and once those are gone it claims iterations from the back of its sibling pieces (high
+// word of theirs). Siblings share the panel, so a stolen iteration adds into the thief's own LDS
+// rows and partial sums; k_sweep_combine adds every piece's partials as before and re-arms the
+// counters. An owner's front claim of iteration S + f and a thief's back claim of n - 1 - b are
+// granted only while S + f + b < n, read from the same 64-bit word by the same atomic add, so no
+// iteration is taken twice or left out. The siblings' column ranges lie on other XCDs (pieces are
+// dealt round-robin), so a stolen iteration gathers x lines its own L2 does not hold: stealing
+// pays only in the tail.
 struct SweepThief {
     uint32_t self, u0, pieces, k;  // own unit, first unit of the panel, pieces, siblings tried
-    uint32_t vic, vn;              // unit claimed from (self while front), its iterations
+    uint32_t vic, vn, vs;          // unit claimed from (self while front), its iterations, its static ones
     uint64_t ve0, ve1;             // its entry range
+    uint32_t tail16;               // claimable share of a unit's iterations, in 16ths
     bool front, end;
 };
+
+// iterations a unit of n keeps without claiming: all but the last tail16/16, at least `ahead`
+__device__ __forceinline__ uint32_t static_iters(uint32_t n, uint32_t tail16, uint32_t ahead)
+{
+    const uint32_t tail = (uint32_t)(((uint64_t)n * tail16 + 15) / 16);
+    return n <= ahead ? n : (n - tail > ahead ? n - tail : ahead);
+}
 
 __device__ __forceinline__ unsigned long long thief_issue(const SweepThief &t, unsigned long long *steal)
 {
@@ -340,17 +349,19 @@ __device__ __forceinline__ unsigned long long thief_issue(const SweepThief &t, u
 __device__ __forceinline__ bool thief_take(const SweepThief &t, unsigned long long old, uint32_t qg, uint32_t ahead,
                                            uint64_t &b, uint64_t &e)
 {
+    (void)ahead;
     const uint32_t f = (uint32_t)old, k = (uint32_t)(old >> 32);
-    if ((uint64_t)ahead + f + k >= t.vn)
+    if ((uint64_t)t.vs + f + k >= t.vn)
         return false;
-    const uint32_t it = t.front ? ahead + f : t.vn - 1 - k;
+    const uint32_t it = t.front ? t.vs + f : t.vn - 1 - k;
     b = t.ve0 + (uint64_t)it * qg;
     e = t.ve1;
     return true;
 }
 
 // the next sibling piece (cyclic after this unit), or the end
-__device__ __forceinline__ void thief_next(SweepThief &t, const uint32_t *__restrict__ unit_ent, uint32_t qg)
+__device__ __forceinline__ void thief_next(SweepThief &t, const uint32_t *__restrict__ unit_ent, uint32_t qg,
+                                           uint32_t ahead)
 {
     t.front = false;
     if (++t.k >= t.pieces) {
@@ -361,6 +372,7 @@ __device__ __forceinline__ void thief_next(SweepThief &t, const uint32_t *__rest
     t.ve0 = unit_ent[t.vic];
     t.ve1 = unit_ent[t.vic + 1];
     t.vn = (uint32_t)((t.ve1 - t.ve0 + qg - 1) / qg);
+    t.vs = static_iters(t.vn, t.tail16, ahead);
 }
 
 // claims until a task is granted (true) or none is left anywhere (false)
@@ -370,7 +382,7 @@ __device__ bool thief_claim_sync(SweepThief &t, unsigned long long *steal, const
     while (!t.end) {
         if (thief_take(t, thief_issue(t, steal), qg, ahead, b, e))
             return true;
-        thief_next(t, unit_ent, qg);
+        thief_next(t, unit_ent, qg, ahead);
     }
     return false;
 }
@@ -383,7 +395,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ unit_panel, const uint32_t *__restrict__ panel_unit,
     A *__restrict__ part, uint32_t stride, uint32_t *__restrict__ pcnt, const V *__restrict__ x,
     V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
-    const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal)
+    const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal,
+    uint32_t tail16)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     constexpr uint32_t QG = Q * (uint32_t)kGroup, kRing = 8, kAhead = 3;
     static_assert(!ST || (LAG > 0 && LAG < (int)kAhead && kAhead + LAG + 1 <= kRing), "steal ring sizing");
     __shared__ uint32_t ring_b[ST ? kRing : 1], ring_e[ST ? kRing : 1], ring_s[ST ? kRing : 1];
-    SweepThief th{blockIdx.x, 0, pieces, 0, blockIdx.x, 0, e0, e1, true, true};
+    SweepThief th{blockIdx.x, 0, pieces, 0, blockIdx.x, 0, 0, e0, e1, tail16, true, true};
     ABL_WG_STAMP(0);
     ABL_WG_IDS();
     for (uint32_t i = threadIdx.x; i <= R; i += T)
@@ -412,10 +425,11 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         if (threadIdx.x == 0) {
             th.u0 = panel_unit[p];
             th.vn = (uint32_t)((e1 - e0 + QG - 1) / QG);
+            th.vs = static_iters(th.vn, tail16, kAhead);
             th.end = false;
             for (uint32_t t = 0; t < kAhead; ++t) {  // the unit's first tasks are its own
                 uint64_t b = 0, e = 0;
-                bool got = t < th.vn;
+                bool got = t < th.vs;
                 if (got)
                     b = e0 + (uint64_t)t * QG, e = e1;
                 else
@@ -436,11 +450,12 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     bool issued = false;
     for (uint32_t s = 0;; ++s) {
         if constexpr (ST) {
-            if (threadIdx.x == 0 && !th.end) {  // its result is consumed after this task's gathers
+            // task s + kAhead: one of the unit's static iterations, or a claim issued here whose
+            // result is consumed after this task's gathers
+            issued = false;
+            if (threadIdx.x == 0 && !th.end && !(th.front && s + kAhead < th.vs)) {
                 pend = thief_issue(th, steal);
                 issued = true;
-            } else {
-                issued = false;
             }
             const uint32_t slot = s % kRing;
             // written kAhead tasks ago unless thread 0 is in a claim loop (the tail); bounded wait
@@ -581,9 +596,13 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
                 if (issued) {
                     got = thief_take(th, pend, QG, kAhead, b, e);
                     if (!got) {
-                        thief_next(th, unit_ent, QG);
+                        thief_next(th, unit_ent, QG, kAhead);
                         got = thief_claim_sync(th, steal, unit_ent, QG, kAhead, b, e);
                     }
+                } else if (!th.end && th.front && s + kAhead < th.vs) {
+                    got = true;
+                    b = e0 + (uint64_t)(s + kAhead) * QG;
+                    e = e1;
                 }
                 const uint32_t slot = (s + kAhead) % kRing;
                 ring_b[slot] = got ? (uint32_t)b : 0xFFFFFFFFu;
@@ -1105,12 +1124,12 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr, \
-                       (unsigned long long *)nullptr)
+                       (unsigned long long *)nullptr, 0u)
     // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
-#define PKD(ST)                                                                                       \
+#define PKD(ST, TAIL)                                                                                 \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
-                       p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr)
+                       p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr, (uint32_t)(TAIL))
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
@@ -1145,11 +1164,13 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 35: PK(2, 2); break;  // variant 28 on the 12-byte rc words of a delta plan (A/B)
         default:
             if (p.sweep_delta) {
-                // split plans steal iterations among a panel's pieces; variant 36 = the static split
+                // split plans steal iterations among a panel's pieces (the last quarter of each
+                // unit's iterations claimable; variants 37 / 38: half / all of them); variant 36 =
+                // the static split
                 if (p.sweep_steal && p.sweep_variant != 36) {
-                    PKD(true);
+                    PKD(true, p.sweep_variant == 37 ? 8 : p.sweep_variant == 38 ? 16 : 4);
                 } else {
-                    PKD(false);
+                    PKD(false, 0);
                 }
             } else {
                 PK(2, 2);
