@@ -108,8 +108,8 @@ typedef struct spmv_plan_stats {
                                     entries; bit 2: lane-ordered chunks (kernel 2); bit 5: row-
                                     sorted segments with 1-byte row deltas (kernel 6); bit 6:
                                     delta-coded columns, 11-byte fp64 / 7-byte fp32 sweep entries
-                                    (kernel 2); bit 7: panels cut into pieces that steal
-                                    iterations from each other (kernel 2, split plans) */
+                                    (kernel 2); bit 7: the tools library's work-stealing
+                                    variants 37-39 are selected (kernel 2, split plans) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are
@@ -139,10 +139,8 @@ int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
  * 26-34 = no barrier, waves run at most 1-4 iterations ahead of the slowest wave of the
  * workgroup (26: 4 groups lag 1, 27: 4/2, 28: 2/2 = default, 29: 2/4, 30: 2/1, 31: 3/2,
  * 32: 1/2, 33: 1/4, 34: 2/3; on a plan with delta-coded columns, stats format bit 6, the default
- * reads 11-byte entries and 35 runs it on the 12-byte words instead; on a split plan, whose
- * panels are cut into pieces, the default steals iterations among a panel's pieces -- the last
- * quarter of each piece's are claimable; 37 / 38: half / all of them -- and 36 keeps the static
- * split); 50-63: measurement-only ablations of the tools library, refused
+ * reads 11-byte entries and 35 runs it on the 12-byte words instead; 36 = the default; 37-39:
+ * measurement-only work stealing among a split plan's pieces, tools library only); 50-63: measurement-only ablations of the tools library, refused
  * here (binned: 51-52). 94 (packed or unpacked): the deterministic kernel of
  * SPMV_SWEEP_DETERMINISTIC=1 (LDS adds in a fixed order, bitwise reproducible y; each wave's
  * adds complete before a release hand-over); 91: the same with a compiler-ordered hand-over

@@ -874,7 +874,8 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
                  (p->kernel == kKernelSlices && p->slice_off_bytes == 1 ? 8 : 0) | (p->tile_col_bytes < 4 ? 1 : 0) | (p->sweep_packed ? 2 : 0) | (p->sweep_lane_order ? 4 : 0) | (p->sweep_delta ? 64 : 0) |
                  (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0) |
                  (p->kernel == kKernelBinned && p->b_delta ? 32 : 0) |
-                 (p->kernel == kKernelSweep && p->sweep_steal && p->sweep_variant != 36 ? 128 : 0);
+                 (p->kernel == kKernelSweep && p->sweep_steal &&
+                          (p->sweep_variant == 37 || p->sweep_variant == 38 || p->sweep_variant == 39) ? 128 : 0);
     return 0;
 }
 
@@ -887,17 +888,17 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
 #ifndef SPMV_ABLATIONS
     // the measurement-only ablations (some give a wrong y by design) exist only in the tools
     // library built with -DSPMV_ABLATIONS (Makefile target `ablations`, tools/ab_variants.py)
-    if ((p->kernel == kKernelSweep && variant >= 50 && variant <= 63) || (p->kernel == kKernelBlocked && variant == 1) ||
+    if ((p->kernel == kKernelSweep && ((variant >= 50 && variant <= 63) || (variant >= 37 && variant <= 39))) ||
+        (p->kernel == kKernelBlocked && variant == 1) ||
         (p->kernel == kKernelBinned && variant >= 51 && variant <= 52)) {
         set_error("spmv_plan_set_variant: measurement-only ablation variant (tools library only)");
         return 1;
     }
 #endif
     if (p->kernel == kKernelSweep) {
-        // every variant but the default (28) and 36-38 (the default with the static split, or with
-        // half / all of each unit's iterations claimable) reads the 12-byte rc words, which a
-        // delta plan rebuilds on first use
-        if ((variant < 36 || variant > 38) && variant != 28 && sweep_materialize_rc(*p))
+        // every variant but the default (28), 36 (the same) and the measurement build's stealing
+        // variants 37-39 reads the 12-byte rc words, which a delta plan rebuilds on first use
+        if ((variant < 36 || variant > 39) && variant != 28 && sweep_materialize_rc(*p))
             return 1;
         p->sweep_variant = variant;
     } else if (p->kernel == kKernelBinned) {

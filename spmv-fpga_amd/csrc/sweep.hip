@@ -313,7 +313,8 @@ __device__ unsigned long long g_abl_wg[4 * 4096];
     do {             \
     } while (0)
 #endif
-// Work stealing among the pieces of a panel (split plans, ST): a unit's workgroup iterations are
+// Work stealing among the pieces of a panel (split plans, ST; measurement build only, variants
+// 37-39 -- it lost 3.5-5.5 % to the static split): a unit's workgroup iterations are
 // tasks. Its first S = static_iters(n) tasks are its own (all but the last tail16/16 of them, at
 // least kAhead); the rest it claims one at a time from the front of its counter (steal[u], low
 // word), and once those are gone it claims iterations from the back of its sibling pieces (high
@@ -1164,14 +1165,17 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 35: PK(2, 2); break;  // variant 28 on the 12-byte rc words of a delta plan (A/B)
         default:
             if (p.sweep_delta) {
-                // split plans steal iterations among a panel's pieces (the last quarter of each
-                // unit's iterations claimable; variants 37 / 38: half / all of them); variant 36 =
-                // the static split
-                if (p.sweep_steal && p.sweep_variant != 36) {
+#ifdef SPMV_ABLATIONS
+                // measurement build: work stealing among a panel's pieces on split plans (the
+                // last quarter / half / all of each piece's iterations claimable: variants 39 / 37
+                // / 38). Measured 3.5-5.5 % slower than the static split at N = 4 and N = 8
+                // (profiles/r04c_steal_ab.jsonl), so the product keeps the static split
+                if (p.sweep_steal && (p.sweep_variant == 37 || p.sweep_variant == 38 || p.sweep_variant == 39)) {
                     PKD(true, p.sweep_variant == 37 ? 8 : p.sweep_variant == 38 ? 16 : 4);
-                } else {
-                    PKD(false, 0);
+                    break;
                 }
+#endif
+                PKD(false, 0);
             } else {
                 PK(2, 2);
             }
@@ -1383,9 +1387,11 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     p.nunits = U;
     if (multi) {
         SPMV_TRY(hipMalloc((void **)&p.d_part, (uint64_t)U * (uint64_t(rmax_used) + 1) * acc));
-        // work-stealing counters (zero; every k_sweep_combine re-arms them)
+#ifdef SPMV_ABLATIONS
+        // work-stealing counters of the measurement variants (zero; every k_sweep_combine re-arms them)
         SPMV_TRY(hipMalloc((void **)&p.d_steal, (uint64_t)U * 8));
         SPMV_TRY(hipMemsetAsync(p.d_steal, 0, (uint64_t)U * 8, s));
+#endif
         // env SPMV_SWEEP_COMBINE=fused: the last piece of each panel combines inside the sweep
         // launch instead of k_sweep_combine. Measured slower on the N = 8 slice of the 10M/160M
         // matrix (0.147 vs 0.128 ms, profiles/r03_ab_sweep_combine.jsonl): the panels of a one-round
@@ -1552,8 +1558,8 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                     (void)hipFree(d_sidx);
                     SW_TRY(e);
                     p.sweep_delta = true;
-                    // split plans run the default kernel with work stealing among a panel's pieces
-                    // (the separate combine kernel re-arms the counters)
+                    // split plans can run the measurement build's work-stealing variants (the separate
+                    // combine kernel re-arms the counters)
                     p.sweep_steal = p.sweep_split > 1 && p.d_steal && !p.d_panel_cnt;
                     // the default kernel reads only the 11-byte entries: the rc words are freed
                     // (rebuilt by sweep_materialize_rc for a variant that reads them)
