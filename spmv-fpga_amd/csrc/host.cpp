@@ -155,9 +155,13 @@ int spmv_mgpu_schedule(int exchange, int rank, int nranks, const IndexType *boun
         set_error("spmv_mgpu_schedule: bad arguments");
         return -1;
     }
+    if (bounds[0] != 0) {
+        set_error("spmv_mgpu_schedule: bounds must start at 0");
+        return -1;
+    }
     for (int r = 0; r < nranks; ++r)
-        if (bounds[r + 1] < bounds[r] || bounds[0] != 0) {
-            set_error("spmv_mgpu_schedule: bounds must start at 0 and be non-decreasing");
+        if (bounds[r + 1] < bounds[r]) {
+            set_error("spmv_mgpu_schedule: bounds must be non-decreasing");
             return -1;
         }
     int n = 0;

@@ -225,13 +225,17 @@ struct XBufs {
     }
 };
 
-// the schedule of local device d's rank for one step
-static std::vector<spmv_xop> schedule_of(const spmv_mgpu *mg, int d, int exchange)
+// the schedule of local device d's rank for one step (1: the handle's bounds were refused)
+static int schedule_of(const spmv_mgpu *mg, int d, int exchange, std::vector<spmv_xop> &ops)
 {
-    std::vector<spmv_xop> ops(2 + 2 * size_t(mg->nranks));
+    ops.resize(2 + 2 * size_t(mg->nranks));
     const int n = spmv_mgpu_schedule(exchange, mg->rank[d], mg->nranks, mg->bounds.data(), ops.data(), (int)ops.size());
-    ops.resize(n < 0 ? 0 : std::min<size_t>(n, ops.size()));
-    return ops;
+    if (n < 0 || size_t(n) > ops.size()) {
+        set_error("spmv_mgpu: no exchange schedule for this handle's slices");
+        return 1;
+    }
+    ops.resize(n);
+    return 0;
 }
 
 static bool has_exchange(const std::vector<spmv_xop> &ops)
@@ -373,8 +377,8 @@ int spmv_mgpu_create_rank(spmv_mgpu **out, int rank, int nranks, const unsigned 
     }
     *out = nullptr;
     for (int r = 0; r < nranks; ++r)
-        if (bounds[r + 1] < bounds[r]) {
-            set_error("spmv_mgpu_create_rank: bounds must be non-decreasing");
+        if (bounds[r + 1] < bounds[r] || bounds[0] != 0) {
+            set_error("spmv_mgpu_create_rank: bounds must start at 0 and be non-decreasing");
             return 1;
         }
     if (plan->nr_rows != bounds[rank + 1] - bounds[rank] || plan->nr_cols != nr_cols || plan->device != device) {
@@ -577,7 +581,8 @@ int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev)
     std::vector<std::vector<spmv_xop>> sch(nl);
     bool any = false;
     for (int d = 0; d < nl; ++d) {
-        sch[d] = schedule_of(mg, d, exchange);
+        if (schedule_of(mg, d, exchange, sch[d]))
+            return 1;
         any = any || has_exchange(sch[d]);
     }
     auto bufs = [&](int d) { return XBufs{mg->y[d], mg->yslice[d], mg->ypart[d], mg->xnext[d]}; };
@@ -682,7 +687,8 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
     std::vector<std::vector<spmv_xop>> sch(nl);
     bool any = false;
     for (int d = 0; d < nl; ++d) {
-        sch[d] = schedule_of(mg, d, exchange);
+        if (schedule_of(mg, d, exchange, sch[d]))
+            return 1;
         any = any || has_exchange(sch[d]);
     }
     for (int d = 0; d < nl; ++d) {
@@ -748,7 +754,9 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
 // RCCL calls only)
 static int enqueue_step(spmv_mgpu *mg, int exchange, const ValueType *x_in, ValueType *x_out, hipStream_t s)
 {
-    const std::vector<spmv_xop> ops = schedule_of(mg, 0, exchange);
+    std::vector<spmv_xop> ops;
+    if (schedule_of(mg, 0, exchange, ops))
+        return 1;
     const XBufs b{mg->y[0], mg->yslice[0], mg->ypart[0], x_out};
     if (issue_local(mg, 0, ops, b, x_in, s))
         return 1;
