@@ -28,6 +28,7 @@ for s in $STEPS; do
     tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     tests_sel) run pytest_sel 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     selflaunch) SPMV_BENCH_BACKEND=gloo run selflaunch_strong 600 python bench.py --gpus 2 --steps 5 --warmup 2 ;;
+    selflaunch4) SPMV_BENCH_BACKEND=gloo run selflaunch4_strong 900 python bench.py --gpus 4 --steps 5 --warmup 2 --no-weak-companion ;;
     selflaunch_weak) SPMV_BENCH_BACKEND=gloo run selflaunch_weak 600 python bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak ;;
     abmirror) run abmirror 900 python tools/ab_variants.py --workload powerlaw --dtype f32 --rounds ${AB_ROUNDS:-7} --reps 10 \
                 --variants binned#1:0,binned#1:7,binned#2:0,binned#2:7,binned#3:0,binned#3:7,binned#4:0,binned#4:7 ;;
