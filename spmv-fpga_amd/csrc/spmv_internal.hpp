@@ -136,10 +136,10 @@ struct spmv_plan {
     uint32_t *d_unit_panel = nullptr;  // panel of each work unit
     uint32_t *d_panel_unit = nullptr;  // first unit of each panel [npanels + 1]
     void *d_part = nullptr;            // split > 1: nunits x (panel_rmax + 1) partial sums (accumulator type)
-    unsigned long long *d_steal = nullptr;  // split > 1: per unit, iterations claimed from the front
-                                            // (low word) and back (high word) -- work stealing among
-                                            // a panel's pieces; re-armed by k_sweep_combine
-    bool sweep_steal = false;          // the default kernel steals (variant 36: the static split)
+    unsigned long long *d_steal = nullptr;  // tools build, split > 1: per unit, iterations claimed
+                                            // from the front (low word) and back (high word) by the
+                                            // work-stealing variants 37-39; re-armed by k_sweep_combine
+    bool sweep_steal = false;          // the stealing variants can run on this plan (tools build)
     uint32_t *d_panel_cnt = nullptr;   // split > 1 with env SPMV_SWEEP_COMBINE=fused: per-panel count of
                                        // finished pieces (the last one combines, sweep.hip
                                        // write_panel); null (default): k_sweep_combine
