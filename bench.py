@@ -757,6 +757,9 @@ def main():
     plan.set_timing(False)
     eager_ms = spmv_dist.max_over_ranks((t1 - t0) * 1e3 / args.steps, dev)
     kernel_ms_max = spmv_dist.max_over_ranks(kernel_ms, dev)
+    per_rank = [0.0] * world  # every rank's dominant-kernel time (load balance of the slices)
+    per_rank[rank] = kernel_ms
+    kernel_ms_ranks = spmv_dist.sum_over_ranks(per_rank, dev) if world > 1 else [kernel_ms]
 
     # 2) the headline: the same K steps replayed from one hipGraph (spmv_plan_run_graph, captured
     #    and warmed once, untimed) -- no host launch gap between steps
@@ -905,6 +908,7 @@ def main():
                      "frac_traffic": (round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
                                       if traffic and kernel_ms > 0 else None),
                      "kernel": kname, "kernel_ms": round(kernel_ms, 5), "l2": l2,
+                     "kernel_ms_per_rank": [round(v, 5) for v in kernel_ms_ranks],
                      "kernel_launches": launches, "alg_bytes_per_launch": alg_local},
         "cpu_baseline": None,
         "parity": None,
