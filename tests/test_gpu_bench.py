@@ -1,0 +1,55 @@
+"""The bench contract on the GPU (bench.py is what the driver runs at N = 1 and N = 2/4/8):
+small power-law matrices through `python bench.py` exactly as the driver calls it, checking the
+JSON line's fields, its own parity, and -- for N = 2 -- the self-launch (no torchrun) with the
+slices gathered on rank 0 and checked against the oracle (main.cpp:77-82 checks every result).
+The two ranks share the box's one GPU over gloo (the rehearsal of the driver's SCALE runs)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+SMALL = ["--rows", "400000", "--nnz", "6400000", "--steps", "3", "--warmup", "1", "--extras-timeout", "150"]
+
+
+def _bench(*args, env=None):
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, *args], capture_output=True,
+                       text=True, timeout=280, env=e, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return lines[0]
+
+
+def test_bench_one_gpu_line():
+    d = _bench("--no-side-configs", "--no-xtiles", "--no-det", "--cpu-reps", "1")
+    assert d["metric"] == "SpMV GFLOP/s + effective HBM GB/s (% roofline), fp64, 1/2/4/8 MI355X"
+    assert d["n_gpus"] == 1 and d["n_ranks"] == 1 and d["steps"] == 3 and d["value"] > 0
+    assert d["config"]["workload"] == "powerlaw" and d["config"]["nnz"] == 6_400_000
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2 and r["kernel_ms"] > 0
+    assert r["kernel_ms_per_rank"] == [r["kernel_ms"]]
+    assert d["cpu_baseline"]["cores"] == 1 and d["cpu_baseline"]["kind"] == "port"
+    assert d["parity"]["pass"] and d["parity"]["max_scaled_err"] <= 1e-12
+
+
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_two_ranks_self_launched(scaling):
+    d = _bench("--gpus", "2", "--scaling", scaling, "--no-weak-companion", "--no-strong-companion",
+               "--no-native-exchange", env={"SPMV_BENCH_BACKEND": "gloo"})
+    assert d["n_gpus"] == 2 and d["n_ranks"] == 2 and d["launcher"] == "bench.py" and d["scaling"] == scaling
+    p = d["parity"]
+    assert p["pass"] and p["max_scaled_err"] <= 1e-12 and p["ref_abs_1e-5_errors"] == 0
+    assert p["rows_checked"] == (400_000 if scaling == "strong" else 800_000)
+    assert len(d["roofline"]["kernel_ms_per_rank"]) == 2
+    if scaling == "strong":
+        assert d["config"]["slice_rows"][0] == 0
+        assert d["exchange"]["backend"] == "gloo" and d["exchange"]["pipelined_max_rel_diff"] == 0.0
