@@ -5,6 +5,7 @@ slices gathered on rank 0 and checked against the oracle (main.cpp:77-82 checks 
 The two ranks share the box's one GPU over gloo (the rehearsal of the driver's SCALE runs)."""
 import json
 import os
+import signal
 import subprocess
 import sys
 
@@ -21,11 +22,18 @@ def _bench(*args, env=None):
     e = {k: v for k, v in os.environ.items()
          if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     e.update(env or {})
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, *args], capture_output=True,
-                       text=True, timeout=280, env=e, cwd=ROOT)
-    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
-    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout[-2000:]
+    # its own process group: on a timeout the self-launched ranks go with the parent
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, *args], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True, env=e, cwd=ROOT, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=280)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        pytest.fail("bench.py timed out: " + err[-4000:])
+    assert p.returncode == 0, out[-2000:] + err[-4000:]
+    lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
     return lines[0]
 
 
