@@ -486,12 +486,16 @@ def side_config(args, name, dev, stream):
            "parity": {"max_scaled_err": err, "tol": tol, "pass": bool(err <= tol)}}
     res["roofline"]["traffic"] = None
     if st["kernel"] == 6 and name == "config5":
-        # PMC traffic of the two binned passes on this matrix (profiles/r02_binned_pmc.json)
-        try:
-            pmc = json.load(open(os.path.join(ROOT, "profiles", "r02_binned_pmc.json")))
-            res["roofline"]["traffic"] = pmc["f32"]["hbm_bytes_per_spmv"]
-        except Exception:
-            pass
+        # PMC traffic of the two binned passes on this matrix: the latest summary
+        # (profiles/binned_pmc.json, tools/pmc_binned.py), else round 2's
+        for fn in ("binned_pmc.json", "r02_binned_pmc.json"):
+            try:
+                pmc = json.load(open(os.path.join(ROOT, "profiles", fn)))
+                res["roofline"]["traffic"] = pmc["f32"]["hbm_bytes_per_spmv"]
+                res["roofline"]["traffic_src"] = "profiles/" + fn
+                break
+            except Exception:
+                continue
     elif name == "config2":
         # PMC traffic of this kernel on this matrix (profiles/traffic.json, key banded_f64), used
         # only when it was recorded for the kernel the plan chose

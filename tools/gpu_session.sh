@@ -63,6 +63,10 @@ for s in $STEPS; do
            run pmc_${wl}_f64_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_f64_$c" -o run -- python bench.py --workload $wl --dtype f64 --no-cpu --no-xtiles --no-side-configs --no-det --steps 5 --warmup 1
          done; done
          python tools/pmc_traffic.py "$OUT" --out "$OUT/traffic.json" > /dev/null ;;
+    pmcbin) for c in FETCH_SIZE WRITE_SIZE; do
+           run pmcbin_f32_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmcbin_f32_$c" -o run -- python bench.py --dtype f32 --no-cpu --no-xtiles --no-side-configs --no-det --steps 5 --warmup 1
+         done
+         python tools/pmc_binned.py "$OUT" --out "$OUT/binned_pmc.json" --session "$(basename $OUT)" ;;
     pmcx) i=0; for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM" \
                     "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_BUSY_avr" \
                     "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD"; do
