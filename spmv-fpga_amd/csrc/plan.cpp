@@ -646,7 +646,7 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_steal, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_part2, (void *)d_steal, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, (void *)d_s_row16, (void *)d_s_d8, (void *)d_s_dbase, (void *)d_s_side, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
                       (void *)d_sbase, (void *)d_slice_len, (void *)d_b_val, (void *)d_b_colw, (void *)d_b_rowp,
@@ -659,6 +659,8 @@ spmv_plan::~spmv_plan()
         (void)hipGraphExecDestroy(gexec);
     if (gstream)
         (void)hipStreamDestroy(gstream);
+    if (gstream2)
+        (void)hipStreamDestroy(gstream2);
 }
 
 uint64_t spmv_plan::device_bytes() const
@@ -789,6 +791,73 @@ int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, voi
     return run_impl(p, d_x, d_y, (hipStream_t)stream, p->timing);
 }
 
+// A split sweep plan (panels cut into pieces whose partial sums k_sweep_combine adds) is captured
+// as a DAG instead of a chain: the combine of step k runs on a second capture stream beside the
+// sweep of step k + 1, the steps' partial sums alternate between two buffers, and the sweep of
+// step k + 2 waits for the combine of step k (its buffer). The combine needs no LDS, so its
+// workgroups fit beside the sweep's one 1024-thread workgroup per CU. Every step still computes
+// all of y = A x; the y of the last step is complete when the graph ends. Not for the tools
+// build's stealing variants (the combine re-arms their counters) or the fused combine.
+static bool graph_overlaps(const spmv_plan *p)
+{
+    return p->kernel == kKernelSweep && p->sweep_split > 1 && !p->d_panel_cnt && p->d_part &&
+           !(p->sweep_variant >= 37 && p->sweep_variant <= 39) && !ablation_env("SPMV_GRAPH_SERIAL");
+}
+
+static int capture_overlapped(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int iters)
+{
+    const uint64_t pbytes = p->nunits * (uint64_t(p->panel_rmax) + 1) * p->sweep_acc_bytes;
+    if (!p->d_part2)
+        SPMV_TRY(hipMalloc(&p->d_part2, pbytes));
+    if (!p->gstream2)
+        SPMV_TRY(hipStreamCreateWithFlags(&p->gstream2, hipStreamNonBlocking));
+    std::vector<hipEvent_t> ev(2 * size_t(iters), nullptr);
+    auto destroy = [&] {
+        for (hipEvent_t e : ev)
+            if (e)
+                (void)hipEventDestroy(e);
+    };
+    for (auto &e : ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            destroy();
+            set_error("spmv_plan_run_graph: hipEventCreate failed");
+            return 1;
+        }
+    hipStream_t a = p->gstream, b = p->gstream2;
+    hipError_t e = hipStreamBeginCapture(a, hipStreamCaptureModeRelaxed);
+    for (int k = 0; k < iters && e == hipSuccess; ++k) {
+        void *part = (k & 1) ? p->d_part2 : p->d_part;
+        if (k >= 2)  // this buffer's previous combine is done
+            e = hipStreamWaitEvent(a, ev[2 * (k - 2) + 1], 0);
+        if (e == hipSuccess)
+            e = launch_sweep(*p, d_x, d_y, a, false, 1, part);
+        if (e == hipSuccess)
+            e = hipEventRecord(ev[2 * k], a);
+        if (e == hipSuccess)
+            e = hipStreamWaitEvent(b, ev[2 * k], 0);
+        if (e == hipSuccess)
+            e = launch_sweep(*p, d_x, d_y, b, false, 2, part);
+        if (e == hipSuccess)
+            e = hipEventRecord(ev[2 * k + 1], b);
+    }
+    if (e == hipSuccess)  // join: the last combine (the combines are in order on b)
+        e = hipStreamWaitEvent(a, ev[2 * (iters - 1) + 1], 0);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(a, &g);
+    destroy();
+    if (e != hipSuccess || ec != hipSuccess) {
+        if (g)
+            (void)hipGraphDestroy(g);
+        set_error(std::string("spmv_plan_run_graph: overlapped capture: ") +
+                  hipGetErrorString(e != hipSuccess ? e : ec));
+        return 1;
+    }
+    const hipError_t ei = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    SPMV_TRY(ei);
+    return 0;
+}
+
 int spmv_plan_run_graph(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int iters, void *stream)
 {
     if (!p || iters < 1) {
@@ -804,21 +873,26 @@ int spmv_plan_run_graph(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int 
         }
         if (!p->gstream)
             SPMV_TRY(hipStreamCreateWithFlags(&p->gstream, hipStreamNonBlocking));
-        SPMV_TRY(hipStreamBeginCapture(p->gstream, hipStreamCaptureModeRelaxed));
-        int rc = 0;
-        for (int i = 0; i < iters && !rc; ++i)
-            rc = run_impl(p, d_x, d_y, p->gstream, false);
-        hipGraph_t g = nullptr;
-        const hipError_t ec = hipStreamEndCapture(p->gstream, &g);
-        if (rc) {
-            if (g)
-                (void)hipGraphDestroy(g);
-            return rc;
+        if (iters >= 2 && graph_overlaps(p)) {
+            if (capture_overlapped(p, d_x, d_y, iters))
+                return 1;
+        } else {
+            SPMV_TRY(hipStreamBeginCapture(p->gstream, hipStreamCaptureModeRelaxed));
+            int rc = 0;
+            for (int i = 0; i < iters && !rc; ++i)
+                rc = run_impl(p, d_x, d_y, p->gstream, false);
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(p->gstream, &g);
+            if (rc) {
+                if (g)
+                    (void)hipGraphDestroy(g);
+                return rc;
+            }
+            SPMV_TRY(ec);
+            const hipError_t ei = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            SPMV_TRY(ei);
         }
-        SPMV_TRY(ec);
-        const hipError_t ei = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        SPMV_TRY(ei);
         p->gx = d_x;
         p->gy = d_y;
         p->giters = iters;

@@ -136,6 +136,8 @@ struct spmv_plan {
     uint32_t *d_unit_panel = nullptr;  // panel of each work unit
     uint32_t *d_panel_unit = nullptr;  // first unit of each panel [npanels + 1]
     void *d_part = nullptr;            // split > 1: nunits x (panel_rmax + 1) partial sums (accumulator type)
+    void *d_part2 = nullptr;           // spmv_plan_run_graph: a second partial buffer, so that the combine
+                                       // of step k runs beside the sweep of step k + 1
     unsigned long long *d_steal = nullptr;  // tools build, split > 1: per unit, iterations claimed
                                             // from the front (low word) and back (high word) by the
                                             // work-stealing variants 37-39; re-armed by k_sweep_combine
@@ -201,6 +203,7 @@ struct spmv_plan {
     // spmv_plan_run_graph: `giters` SpMVs on (gx, gy) captured once, replayed per call
     hipGraphExec_t gexec = nullptr;
     hipStream_t gstream = nullptr;
+    hipStream_t gstream2 = nullptr;  // second capture stream (split sweep: the combines)
     const ValueType *gx = nullptr;
     ValueType *gy = nullptr;
     int giters = 0;
@@ -265,7 +268,10 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
                  hipStream_t s);
 
 // sweep.hip
-hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false);
+// phase 0: the sweep and (split plans) the combine; 1: the sweep only; 2: the combine only.
+// part: the partial-sum buffer of a split plan (null: the plan's own d_part)
+hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false,
+                        int phase = 0, void *part = nullptr);
 // 0 ok, 1 error, 2 the padded layout would overflow 32-bit entry offsets (caller may use tiles)
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s);

@@ -1079,11 +1079,12 @@ __global__ void k_locality(const IndexType *__restrict__ rp, const IndexType *__
 }
 
 template <int T, typename A>
-static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
+static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm,
+                           void *part_buf)
 {
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(A);
     const dim3 grid((unsigned)p.nunits), block(T);
-    A *part = reinterpret_cast<A *>(p.d_part);
+    A *part = reinterpret_cast<A *>(part_buf);
     uint32_t *pcnt = p.sweep_split > 1 && p.d_panel_cnt ? p.d_panel_cnt : nullptr;  // fused combine
     // Unpacked (14-B entries, used when a chunk spans >= 65536 columns): E entries per thread,
     // Q groups per barrier, SYNC barrier, NT non-temporal entry loads.
@@ -1200,31 +1201,37 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 }
 
 template <typename A>
-static void launch_sweep_a(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
+static void launch_sweep_a(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm,
+                           int phase, void *part)
 {
-    switch (p.sweep_threads) {
-    case 256: launch_sweep_t<256, A>(p, d_x, d_y, s, warm); break;
-    case 512: launch_sweep_t<512, A>(p, d_x, d_y, s, warm); break;
-    default: launch_sweep_t<1024, A>(p, d_x, d_y, s, warm); break;
+    if (phase != 2) {
+        switch (p.sweep_threads) {
+        case 256: launch_sweep_t<256, A>(p, d_x, d_y, s, warm, part); break;
+        case 512: launch_sweep_t<512, A>(p, d_x, d_y, s, warm, part); break;
+        default: launch_sweep_t<1024, A>(p, d_x, d_y, s, warm, part); break;
+        }
     }
-    if (p.sweep_split > 1 && !p.d_panel_cnt) {  // env SPMV_SWEEP_COMBINE=kernel
+    if (phase != 1 && p.sweep_split > 1 && !p.d_panel_cnt) {  // the combine kernel (not the fused form)
         const dim3 grid((p.panel_rmax + 255) / 256, (unsigned)p.npanels);
         launch_or_warm(warm, k_sweep_combine<ValueType, A>, grid, dim3(256), 0, s, p.d_panel_row, p.d_panel_unit,
-                       reinterpret_cast<const A *>(p.d_part), p.panel_rmax + 1, d_y, p.d_steal);
+                       reinterpret_cast<const A *>(part), p.panel_rmax + 1, d_y, p.d_steal);
     }
 }
 
-hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm)
+hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm, int phase,
+                        void *part)
 {
     if (p.npanels == 0)
         return hipSuccess;
+    if (!part)
+        part = p.d_part;
     if constexpr (sizeof(ValueType) == 4) {
         if (p.sweep_acc_bytes == 4) {
-            launch_sweep_a<float>(p, d_x, d_y, s, warm);
+            launch_sweep_a<float>(p, d_x, d_y, s, warm, phase, part);
             return hipGetLastError();
         }
     }
-    launch_sweep_a<double>(p, d_x, d_y, s, warm);
+    launch_sweep_a<double>(p, d_x, d_y, s, warm, phase, part);
     return hipGetLastError();
 }
 

@@ -140,3 +140,37 @@ def test_distinct_plans_run_concurrently_on_two_streams(torch, dtype):
         err = oracle.scaled_error(rp_h, c_h, v_h, x_h, ref, y.cpu().numpy())
         assert err <= TIGHT[np.dtype(dtype)], (p.stats()["kernel"], err)
         p.destroy()
+
+
+@pytest.mark.parametrize("iters", [1, 2, 3, 6])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_run_graph_overlaps_the_split_combine(torch, monkeypatch, dtype, iters):
+    """A split sweep plan (rank 0 of the N = 8 cut of the 10M/160M matrix: panels cut into
+    pieces, partial sums added by k_sweep_combine) is captured as a DAG: the combine of step k
+    beside the sweep of step k + 1, two partial buffers. y after the replay (and after a second
+    replay, and a fresh x through a re-capture) matches the oracle, as with the serial capture of
+    the tools build (SPMV_GRAPH_SERIAL=1)."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    n = 10_000_000
+    for ablations in (False, True):
+        if ablations:
+            monkeypatch.setenv("SPMV_GRAPH_SERIAL", "1")
+        lib = spmv_hw.load(dtype, ablations=ablations)
+        rp_full, _ = lib.powerlaw_row_ptr(n, 160_000_000, 65536, 4)
+        b = lib.partition_rows(rp_full, 8)
+        r0, r1 = int(b[0]), int(b[1])
+        rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 160_000_000, seed=4, row_begin=r0, row_end=r1)
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+        assert plan.stats()["nr_tiles"] > 200  # split: ~62 panels in ~4 pieces each
+        h = _host(rp, col, val)
+        r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+        for seed in (6, 7):  # a new x buffer re-captures the graph
+            x = spmv_hw.gen_vector(lib, n, seed=seed, lo=-1.0 if seed == 7 else 0.0)
+            ref = (oracle.spmv_fp64acc if dtype == np.float32 else oracle.spmv_gold)(r, c, h[2], x.cpu().numpy())
+            y = torch.full((r1 - r0,), float("nan"), dtype=x.dtype, device="cuda")
+            for _ in range(2):  # capture + replay, then a second replay
+                plan.run_graph(x, y, iters)
+                torch.cuda.synchronize()
+                err = oracle.scaled_error(r, c, h[2], x.cpu().numpy(), ref, y.cpu().numpy())
+                assert err <= TIGHT[np.dtype(dtype)], (ablations, seed, err)
+        plan.destroy()

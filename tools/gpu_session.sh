@@ -33,6 +33,7 @@ for s in $STEPS; do
     abmirror) run abmirror 900 python tools/ab_variants.py --workload powerlaw --dtype f32 --rounds ${AB_ROUNDS:-7} --reps 10 \
                 --variants binned#1:0,binned#1:7,binned#2:0,binned#2:7,binned#3:0,binned#3:7,binned#4:0,binned#4:7 ;;
     absteal) run absteal 900 python tools/strong_slices.py --ns ${STEAL_NS:-4,8} --slices all --variants ${STEAL_VARIANTS:-28,36,37,38} --rounds ${AB_ROUNDS:-5} --reps 20 ;;
+    abgraph) run abgraph 900 python tools/strong_slices.py --ns ${GRAPH_NS:-4,8} --slices all --graph-ab ${GRAPH_K:-20} --rounds ${AB_ROUNDS:-5} ;;
     tests_all) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
