@@ -1030,7 +1030,9 @@ def main():
         res["e2e_gflops_with_reduce"] = round(2.0 * nnz_all / ((ms + res["reduce_ms"]) * 1e-3) / 1e9, 2)
         res["e2e_gflops_with_allgather"] = round(2.0 * nnz_all / ((ms + res["allgather_ms"]) * 1e-3) / 1e9, 2)
         res["backend"] = dist.get_backend()
-        if not args.no_native_exchange:
+        if world > torch.cuda.device_count():  # the single-GPU rehearsal: ranks share a device
+            res["native"] = {"skipped": "ranks share one GPU; RCCL refuses two ranks on one device"}
+        elif not args.no_native_exchange:
             try:
                 res["native"] = native_exchange(lib, plan, x, st["nr_cols"], counts, world, rank, dev)
             except Exception as e:  # reported, never fatal to the bench line
