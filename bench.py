@@ -90,6 +90,10 @@ def parse(argv=None):
                     help="N > 1: skip the library's own RCCL exchange (spmv_mgpu_create_rank)")
     ap.add_argument("--no-side-configs", action="store_true",
                     help="1 GPU: skip the config-2 (banded fp64) and config-5 (power-law fp32) side lines")
+    ap.add_argument("--dist-rehearsal", action="store_true",
+                    help="1 GPU: run the N > 1 code path as the one rank of an RCCL ('nccl') process "
+                         "group -- its collectives, parity gather, exchange fields and the library's "
+                         "own clique on the hardware (the path of the 8-GPU run, at world size 1)")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the row-parallel CPU line (the box's CPU share is 16)")
@@ -103,8 +107,11 @@ def parse(argv=None):
                     help="with --dry-launch: RANK:RC[,RANK:RC] exit codes of those ranks (launcher tests; "
                          "RC < 0 kills the rank with signal -RC, 'hang' makes it sleep)")
     a = ap.parse_args(argv)
+    if a.dist_rehearsal and a.gpus != 1:
+        ap.error("--dist-rehearsal is the one-GPU form of the N > 1 path")
     if a.scaling is None:
         a.scaling = "strong" if a.gpus > 1 else "weak"
+    a.multi = a.gpus > 1 or a.dist_rehearsal  # the N > 1 path: a process group, slices, exchange
     return a
 
 
@@ -199,7 +206,12 @@ def setup_dist(args):
         raise SystemExit(f"{world} ranks but only {ndev} GPUs (use SPMV_BENCH_BACKEND=gloo to rehearse)")
     dev_index = local % ndev
     torch.cuda.set_device(dev_index)
-    if world > 1:
+    if args.dist_rehearsal:  # one rank, its own rendezvous (no launcher around it)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if args.multi:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
@@ -208,7 +220,7 @@ def setup_dist(args):
 
 
 def barrier(world):
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
 
 
@@ -222,7 +234,7 @@ def build_workload(lib, args, world, rank):
         return rp, col, val, x, n, desc
     n = args.rows or 10_000_000
     z = args.nnz or 160_000_000
-    if world > 1 and args.scaling == "strong":
+    if args.multi and args.scaling == "strong":
         rp_full, _ = lib.powerlaw_row_ptr(n, z, 65536, 4)
         b = lib.partition_rows(rp_full, world)
         r0, r1 = spmv_dist.row_slice(b, rank)
@@ -738,8 +750,8 @@ def main():
     y = torch.empty(st["nr_rows"], dtype=x.dtype, device=dev)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
-    keep_csr = rank == 0 and world == 1 and not args.no_cpu
-    want_xtiles = world == 1 and args.workload == "powerlaw" and not args.no_xtiles
+    keep_csr = rank == 0 and not args.multi and not args.no_cpu
+    want_xtiles = not args.multi and args.workload == "powerlaw" and not args.no_xtiles
     if not keep_csr and not want_xtiles:
         del rp, col, val
         torch.cuda.empty_cache()
@@ -765,7 +777,7 @@ def main():
     kernel_ms_max = spmv_dist.max_over_ranks(kernel_ms, dev)
     per_rank = [0.0] * world  # every rank's dominant-kernel time (load balance of the slices)
     per_rank[rank] = kernel_ms
-    kernel_ms_ranks = spmv_dist.sum_over_ranks(per_rank, dev) if world > 1 else [kernel_ms]
+    kernel_ms_ranks = spmv_dist.sum_over_ranks(per_rank, dev) if args.multi else [kernel_ms]
 
     # 2) the headline: the same K steps replayed from one hipGraph (spmv_plan_run_graph, captured
     #    and warmed once, untimed) -- no host launch gap between steps
@@ -820,7 +832,7 @@ def main():
     nnz_local = st["nr_nzeros"]
     alg_local = st["algorithmic_bytes"]
     nnz_all, alg_all = spmv_dist.sum_over_ranks([float(nnz_local), float(alg_local)], dev)
-    if world > 1 and args.scaling == "strong":
+    if args.multi and args.scaling == "strong":
         # one matrix: x and the row_ptr sentinel count once, not once per rank
         alg_all -= (world - 1) * (st["nr_cols"] * np.dtype(dtype).itemsize + 4)
 
@@ -896,11 +908,12 @@ def main():
         "n_gpus": world,
         "n_ranks": dist.get_world_size() if dist.is_initialized() else 1,
         "launcher": os.environ.get("SPMV_BENCH_LAUNCHER") or ("torch.distributed.run" if world > 1 else None),
+        "dist_rehearsal": bool(args.dist_rehearsal),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 5),
         "higher_is_better": True,
-        "scaling": args.scaling if world > 1 else "weak",
+        "scaling": args.scaling if args.multi else "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (splitmix64 generator, SURVEY.md §8d)",
@@ -1039,12 +1052,12 @@ def main():
                 res["native"] = {"error": str(e)[:300]}
         return res
 
-    if world > 1:  # correctness first: the parity of this very run, then the side measurements
+    if args.multi:  # correctness first: the parity of this very run, then the side measurements
         guarded("parity", lambda: distributed_parity(lib, args, world, rank, dev, y, st))
         guarded("exchange", exchange_fields)
-    if world > 1 and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
+    if args.multi and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
         guarded("strong_companion", lambda: strong_companion(lib, args, world, rank, dev, stream))
-    if world > 1 and args.scaling == "strong" and args.workload == "powerlaw" and not args.no_weak_companion:
+    if args.multi and args.scaling == "strong" and args.workload == "powerlaw" and not args.no_weak_companion:
         guarded("weak_companion", lambda: weak_companion(lib, args, world, rank, dev, stream))
     if keep_csr:
         def cpu_fields():
@@ -1053,12 +1066,12 @@ def main():
         guarded("cpu_baseline", cpu_fields)
         del rp, col, val
         torch.cuda.empty_cache()
-    if world == 1 and args.workload == "powerlaw" and args.dtype == "f64" and not args.no_side_configs:
+    if not args.multi and args.workload == "powerlaw" and args.dtype == "f64" and not args.no_side_configs:
         guarded("side_configs", lambda: {name: side_config(args, name, dev, stream) for name in ("config2", "config5")})
     watchdog.cancel()
     emit()
     plan.destroy()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -67,3 +67,12 @@ def test_one_gpu_runs_in_process():
     assert p.returncode == 0, p.stderr
     (line,) = _lines(p.stdout)
     assert line["gpus"] == 1 and line["WORLD_SIZE"] is None
+
+
+def test_dist_rehearsal_is_one_gpu_only():
+    """--dist-rehearsal runs the N > 1 path as one rank of an RCCL group (tests/test_gpu_bench.py);
+    it is refused with --gpus > 1, where the real process group takes its place."""
+    p = _run("--gpus", "2", "--dist-rehearsal", "--dry-launch")
+    assert p.returncode == 2 and "one-GPU form" in p.stderr, p.stderr
+    p = _run("--dist-rehearsal", "--dry-launch")
+    assert p.returncode == 0, p.stderr

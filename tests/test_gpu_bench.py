@@ -2,7 +2,9 @@
 small power-law matrices through `python bench.py` exactly as the driver calls it, checking the
 JSON line's fields, its own parity, and -- for N = 2 -- the self-launch (no torchrun) with the
 slices gathered on rank 0 and checked against the oracle (main.cpp:77-82 checks every result).
-The two ranks share the box's one GPU over gloo (the rehearsal of the driver's SCALE runs)."""
+The two ranks share the box's one GPU over gloo (the rehearsal of the driver's SCALE runs); the
+RCCL side of the same path runs as the one rank of an 'nccl' group (--dist-rehearsal): torch's
+collectives on device tensors, the parity gather and the library's own clique."""
 import json
 import os
 import signal
@@ -61,3 +63,20 @@ def test_bench_two_ranks_self_launched(scaling):
     if scaling == "strong":
         assert d["config"]["slice_rows"][0] == 0
         assert d["exchange"]["backend"] == "gloo" and d["exchange"]["pipelined_max_rel_diff"] == 0.0
+
+
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_one_rank_rccl_rehearsal(scaling):
+    d = _bench("--dist-rehearsal", "--scaling", scaling, "--no-weak-companion", "--no-strong-companion")
+    assert d["dist_rehearsal"] and d["n_gpus"] == 1 and d["n_ranks"] == 1 and d["scaling"] == scaling
+    p = d["parity"]
+    assert p["pass"] and p["max_scaled_err"] <= 1e-12 and p["rows_checked"] == 400_000
+    if scaling == "strong":
+        assert d["config"]["slice_rows"] == [0, 400_000]
+        ex = d["exchange"]
+        assert ex["backend"] == "nccl" and ex["pipelined_max_rel_diff"] == 0.0, ex
+        assert all(ex[k] > 0 for k in ("gather_ms", "reduce_ms", "allgather_ms", "x_broadcast_ms"))
+        nat = ex["native"]
+        assert "error" not in nat, nat
+        assert nat["rccl_comm_count"] == 1 and nat["gather_max_rel_diff_vs_torch"] <= 1e-12  # two SpMVs (LDS adds)
+        assert all(nat[k] > 0 for k in ("gather_compute_ms", "reduce_exchange_ms", "allgather_graph_ms_per_step"))
