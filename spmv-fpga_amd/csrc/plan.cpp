@@ -646,13 +646,15 @@ spmv_plan::~spmv_plan()
     (void)hipDeviceSynchronize();
     for (void *ptr : {(void *)d_col, (void *)d_val, (void *)d_rowend, (void *)d_tile_info,
                       (void *)d_row_id, (void *)d_head, (void *)d_tail, (void *)d_cross, (void *)d_s_col,
-                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_part2, (void *)d_steal, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
+                      (void *)d_s_row, (void *)d_s_val, (void *)d_panel_row, (void *)d_unit_ent, (void *)d_part, (void *)d_gcount, (void *)d_steal, (void *)d_panel_cnt, (void *)d_unit_panel, (void *)d_panel_unit, (void *)d_rp,
                       (void *)d_s_cbase, (void *)d_s_row16, (void *)d_s_d8, (void *)d_s_dbase, (void *)d_s_side, d_colnar, (void *)d_tile_cbase, (void *)d_kptr, (void *)d_kpos,
                       (void *)d_rp2, (void *)d_rl, (void *)d_chunk_row, (void *)d_bpart, (void *)d_slot_off,
                       (void *)d_sbase, (void *)d_slice_len, (void *)d_b_val, (void *)d_b_colw, (void *)d_b_rowp,
                       d_b_prod_alloc, (void *)d_b_seg, (void *)d_b_seg_hi, (void *)d_b_ub, (void *)d_b_uwin})
         if (ptr)
             (void)hipFree(ptr);
+    for (void *ptr : gpart)
+        (void)hipFree(ptr);
     for (hipEvent_t e : ev)
         (void)hipEventDestroy(e);
     if (gexec)
@@ -801,14 +803,24 @@ int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, voi
 static bool graph_overlaps(const spmv_plan *p)
 {
     return p->kernel == kKernelSweep && p->sweep_split > 1 && !p->d_panel_cnt && p->d_part &&
-           !(p->sweep_variant >= 37 && p->sweep_variant <= 39) && !ablation_env("SPMV_GRAPH_SERIAL");
+           !(p->sweep_variant >= 37 && p->sweep_variant <= 39);
+}
+
+static int graph_part2(spmv_plan *p)
+{
+    if (p->gpart.empty()) {
+        void *b = nullptr;
+        SPMV_TRY(hipMalloc(&b, p->nunits * (uint64_t(p->panel_rmax) + 1) * p->sweep_acc_bytes));
+        p->gpart.push_back(b);
+    }
+    return 0;
 }
 
 static int capture_overlapped(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int iters)
 {
-    const uint64_t pbytes = p->nunits * (uint64_t(p->panel_rmax) + 1) * p->sweep_acc_bytes;
-    if (!p->d_part2)
-        SPMV_TRY(hipMalloc(&p->d_part2, pbytes));
+    constexpr int R = 2;  // partial buffers (longer rings measured slower)
+    if (graph_part2(p))
+        return 1;
     if (!p->gstream2)
         SPMV_TRY(hipStreamCreateWithFlags(&p->gstream2, hipStreamNonBlocking));
     std::vector<hipEvent_t> ev(2 * size_t(iters), nullptr);
@@ -826,9 +838,9 @@ static int capture_overlapped(spmv_plan *p, const ValueType *d_x, ValueType *d_y
     hipStream_t a = p->gstream, b = p->gstream2;
     hipError_t e = hipStreamBeginCapture(a, hipStreamCaptureModeRelaxed);
     for (int k = 0; k < iters && e == hipSuccess; ++k) {
-        void *part = (k & 1) ? p->d_part2 : p->d_part;
-        if (k >= 2)  // this buffer's previous combine is done
-            e = hipStreamWaitEvent(a, ev[2 * (k - 2) + 1], 0);
+        void *part = k % R ? p->gpart[k % R - 1] : p->d_part;
+        if (k >= R)  // this buffer's previous combine is done
+            e = hipStreamWaitEvent(a, ev[2 * (k - R) + 1], 0);
         if (e == hipSuccess)
             e = launch_sweep(*p, d_x, d_y, a, false, 1, part);
         if (e == hipSuccess)
@@ -858,6 +870,63 @@ static int capture_overlapped(spmv_plan *p, const ValueType *d_x, ValueType *d_y
     return 0;
 }
 
+// The "behind" form (default for split plans whose sweep can carry it, sweep_behind_ok): one
+// stream, one launch per step, and the combine of step k rides in step k + 1's sweep launch as
+// extra blocks that start on the CUs no unit holds and in the sweep's tail (sweep.hip,
+// combine_behind); a last k_sweep_combine finishes the last step. Partials alternate between
+// d_part and gpart[0]. No second stream, so no cross-queue hand-off between the steps.
+static int capture_behind(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int iters)
+{
+    if (graph_part2(p))
+        return 1;
+    if (!p->d_gcount) {
+        SPMV_TRY(hipMalloc(&p->d_gcount, 2 * sizeof(uint32_t)));
+        SPMV_TRY(hipMemset(p->d_gcount, 0, 2 * sizeof(uint32_t)));
+    }
+    int ncu = 0;
+    SPMV_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
+    auto part_of = [&](int k) { return (k & 1) ? p->gpart[0] : p->d_part; };
+    hipStream_t a = p->gstream;
+    hipError_t e = hipStreamBeginCapture(a, hipStreamCaptureModeRelaxed);
+    for (int k = 0; k < iters && e == hipSuccess; ++k) {
+        sweep_behind bh;
+        bh.cpart = k ? part_of(k - 1) : nullptr;
+        bh.ccount = p->d_gcount + (k & 1);
+        bh.cnext = p->d_gcount + ((k + 1) & 1);
+        bh.blocks = (uint32_t)std::max(ncu, 1);
+        e = launch_sweep(*p, d_x, d_y, a, false, 1, part_of(k), &bh);
+    }
+    if (e == hipSuccess)  // the last step's combine
+        e = launch_sweep(*p, d_x, d_y, a, false, 2, part_of(iters - 1));
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(a, &g);
+    if (e != hipSuccess || ec != hipSuccess) {
+        if (g)
+            (void)hipGraphDestroy(g);
+        set_error(std::string("spmv_plan_run_graph: behind capture: ") + hipGetErrorString(e != hipSuccess ? e : ec));
+        return 1;
+    }
+    const hipError_t ei = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    SPMV_TRY(ei);
+    return 0;
+}
+
+// the capture form of a run_graph: 0 serial chain, 1 two-stream DAG, 2 behind. The tools build's
+// SPMV_GRAPH_FORM=serial|dag|behind forces one (where the plan allows it)
+static int graph_form(const spmv_plan *p)
+{
+    const int best = p->kernel == kKernelSweep && sweep_behind_ok(*p) ? 2 : graph_overlaps(p) ? 1 : 0;
+    if (const char *f = ablation_env("SPMV_GRAPH_FORM")) {
+        const std::string v(f);
+        if (v == "serial")
+            return 0;
+        if (v == "dag" && best >= 1)
+            return 1;
+    }
+    return best;
+}
+
 int spmv_plan_run_graph(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int iters, void *stream)
 {
     if (!p || iters < 1) {
@@ -873,7 +942,11 @@ int spmv_plan_run_graph(spmv_plan *p, const ValueType *d_x, ValueType *d_y, int 
         }
         if (!p->gstream)
             SPMV_TRY(hipStreamCreateWithFlags(&p->gstream, hipStreamNonBlocking));
-        if (iters >= 2 && graph_overlaps(p)) {
+        const int form = iters >= 2 ? graph_form(p) : 0;
+        if (form == 2) {
+            if (capture_behind(p, d_x, d_y, iters))
+                return 1;
+        } else if (form == 1) {
             if (capture_overlapped(p, d_x, d_y, iters))
                 return 1;
         } else {

@@ -136,8 +136,9 @@ struct spmv_plan {
     uint32_t *d_unit_panel = nullptr;  // panel of each work unit
     uint32_t *d_panel_unit = nullptr;  // first unit of each panel [npanels + 1]
     void *d_part = nullptr;            // split > 1: nunits x (panel_rmax + 1) partial sums (accumulator type)
-    void *d_part2 = nullptr;           // spmv_plan_run_graph: a second partial buffer, so that the combine
-                                       // of step k runs beside the sweep of step k + 1
+    std::vector<void *> gpart;         // spmv_plan_run_graph: a second partial buffer beside d_part, so
+                                       // that the combine of step k runs beside the sweep of step k + 1
+    uint32_t *d_gcount = nullptr;      // spmv_plan_run_graph, "behind" form: two chunk counters
     unsigned long long *d_steal = nullptr;  // tools build, split > 1: per unit, iterations claimed
                                             // from the front (low word) and back (high word) by the
                                             // work-stealing variants 37-39; re-armed by k_sweep_combine
@@ -270,8 +271,17 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
 // sweep.hip
 // phase 0: the sweep and (split plans) the combine; 1: the sweep only; 2: the combine only.
 // part: the partial-sum buffer of a split plan (null: the plan's own d_part)
+// behind: (spmv_plan_run_graph of a split plan) the previous step's combine, run by extra blocks
+// of this sweep launch (sweep.hip, combine_behind); only where sweep_behind_ok
+struct sweep_behind {
+    const void *cpart = nullptr;  // the previous step's partial sums (null: nothing to combine)
+    uint32_t *ccount = nullptr;   // this launch's chunk counter (zero when it starts)
+    uint32_t *cnext = nullptr;    // zeroed by this launch: the next launch's counter
+    uint32_t blocks = 0;          // extra blocks when cpart is set
+};
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false,
-                        int phase = 0, void *part = nullptr);
+                        int phase = 0, void *part = nullptr, const sweep_behind *behind = nullptr);
+bool sweep_behind_ok(const spmv_plan &p);  // the plan's sweep launch can carry a combine behind
 // 0 ok, 1 error, 2 the padded layout would overflow 32-bit entry offsets (caller may use tiles)
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s);

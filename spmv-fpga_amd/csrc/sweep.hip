@@ -388,6 +388,60 @@ __device__ bool thief_claim_sync(SweepThief &t, unsigned long long *steal, const
     return false;
 }
 
+// The combine of the PREVIOUS step run by extra workgroups of this step's sweep launch
+// (spmv_plan_run_graph of a split plan, the "behind" form): blocks nunits.. of the grid are
+// dispatched after every sweep unit, so they start on the CUs no unit holds and on those whose
+// unit has finished (the sweep's tail). They claim chunks of kBehindRows rows of a panel from
+// *ccount until none is left and add the pieces' partial sums in piece order, as
+// k_sweep_combine does (the same y bit for bit). The previous step's partials (cpart) are not
+// the ones this step's units write, and the rows they store are those of split panels, which the
+// units leave to the partials.
+constexpr uint32_t kBehindRows = 4096;
+template <typename V, int T, typename A>
+__device__ void combine_behind(const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_unit,
+                               const A *__restrict__ cpart, uint32_t stride, V *__restrict__ y,
+                               uint32_t *__restrict__ ccount, uint32_t npanels)
+{
+    constexpr uint32_t J = kBehindRows / T;
+    const uint32_t cpp = (stride + kBehindRows - 1) / kBehindRows;  // chunks per panel
+    __shared__ uint32_t claim;
+    for (;;) {
+        if (threadIdx.x == 0)
+            claim = __hip_atomic_fetch_add(ccount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t c = claim;
+        __syncthreads();
+        if (c >= npanels * cpp)
+            return;
+        const uint32_t p = c / cpp, i0 = (c % cpp) * kBehindRows;
+        const uint32_t u0 = panel_unit[p], pieces = panel_unit[p + 1] - u0;
+        const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
+        if (pieces < 2 || i0 >= R)
+            continue;
+        const A *src = cpart + (uint64_t)u0 * stride;
+        A acc[J];
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint32_t i = i0 + j * T + threadIdx.x;
+            acc[j] = i < R ? src[i] : A(0);
+        }
+        for (uint32_t t = 1; t < pieces; ++t) {
+            const A *sp = src + (uint64_t)t * stride;
+#pragma unroll
+            for (uint32_t j = 0; j < J; ++j) {
+                const uint32_t i = i0 + j * T + threadIdx.x;
+                acc[j] += i < R ? sp[i] : A(0);
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint32_t i = i0 + j * T + threadIdx.x;
+            if (i < R)
+                y[r0 + i] = V(acc[j]);
+        }
+    }
+}
+
 template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double, bool DL = false,
           bool ST = false>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
@@ -397,13 +451,20 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     A *__restrict__ part, uint32_t stride, uint32_t *__restrict__ pcnt, const V *__restrict__ x,
     V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
     const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal,
-    uint32_t tail16)
+    uint32_t tail16, uint32_t nunits, const A *__restrict__ cpart, uint32_t *__restrict__ ccount,
+    uint32_t *__restrict__ cnext, uint32_t npanels)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
     typedef uint8_t u8x2 __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     A *ylds = reinterpret_cast<A *>(smem);
+    if (blockIdx.x >= nunits) {  // the previous step's combine, behind this step's units
+        combine_behind<V, T, A>(panel_row, panel_unit, cpart, stride, y, ccount, npanels);
+        return;
+    }
+    if (cnext && blockIdx.x == 0 && threadIdx.x == 0)  // the next launch's claim counter
+        __hip_atomic_store(cnext, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t p = unit_panel[blockIdx.x];  // unit = a piece of a panel's column-sorted entries
     const uint32_t pieces = panel_unit[p + 1] - panel_unit[p];
     const uint32_t r0 = panel_row[p], R = panel_row[p + 1] - r0;
@@ -1080,10 +1141,11 @@ __global__ void k_locality(const IndexType *__restrict__ rp, const IndexType *__
 
 template <int T, typename A>
 static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm,
-                           void *part_buf)
+                           void *part_buf, const sweep_behind &bh)
 {
     const size_t lds = (size_t(p.panel_rmax) + 1) * sizeof(A);
     const dim3 grid((unsigned)p.nunits), block(T);
+    const dim3 gridb((unsigned)p.nunits + (bh.cpart ? bh.blocks : 0u));  // + the combine behind
     A *part = reinterpret_cast<A *>(part_buf);
     uint32_t *pcnt = p.sweep_split > 1 && p.d_panel_cnt ? p.d_panel_cnt : nullptr;  // fused combine
     // Unpacked (14-B entries, used when a chunk spans >= 65536 columns): E entries per thread,
@@ -1126,12 +1188,13 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr, \
-                       (unsigned long long *)nullptr, 0u)
+                       (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u)
     // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
 #define PKD(ST, TAIL)                                                                                 \
-    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, grid, block, lds, s, p.d_s_col, \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, gridb, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
-                       p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr, (uint32_t)(TAIL))
+                       p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr, (uint32_t)(TAIL), \
+                       (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
@@ -1200,15 +1263,30 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 #undef SWEEP
 }
 
+// the variants launch_sweep_t sends to the default delta kernel (PKD(false, 0)), split plans
+// with the combine kernel: those whose launch can carry the previous step's combine
+bool sweep_behind_ok(const spmv_plan &p)
+{
+    if (!p.sweep_packed || !p.sweep_delta || p.sweep_det || p.sweep_split < 2 || p.d_panel_cnt)
+        return false;
+    switch (p.sweep_variant) {
+    case 15: case 20: case 22: case 26: case 27: case 29: case 30: case 31: case 32: case 33: case 34:
+    case 35: case 37: case 38: case 39: case kSweepTurn: case kSweepTurnOrdered:
+        return false;
+    default:
+        return !(p.sweep_variant >= 50 && p.sweep_variant <= 63);
+    }
+}
+
 template <typename A>
 static void launch_sweep_a(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm,
-                           int phase, void *part)
+                           int phase, void *part, const sweep_behind &bh)
 {
     if (phase != 2) {
         switch (p.sweep_threads) {
-        case 256: launch_sweep_t<256, A>(p, d_x, d_y, s, warm, part); break;
-        case 512: launch_sweep_t<512, A>(p, d_x, d_y, s, warm, part); break;
-        default: launch_sweep_t<1024, A>(p, d_x, d_y, s, warm, part); break;
+        case 256: launch_sweep_t<256, A>(p, d_x, d_y, s, warm, part, bh); break;
+        case 512: launch_sweep_t<512, A>(p, d_x, d_y, s, warm, part, bh); break;
+        default: launch_sweep_t<1024, A>(p, d_x, d_y, s, warm, part, bh); break;
         }
     }
     if (phase != 1 && p.sweep_split > 1 && !p.d_panel_cnt) {  // the combine kernel (not the fused form)
@@ -1219,19 +1297,23 @@ static void launch_sweep_a(const spmv_plan &p, const ValueType *d_x, ValueType *
 }
 
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm, int phase,
-                        void *part)
+                        void *part, const sweep_behind *behind)
 {
     if (p.npanels == 0)
         return hipSuccess;
     if (!part)
         part = p.d_part;
+    const sweep_behind none{};
+    if (behind && (behind->cpart || behind->cnext) && !sweep_behind_ok(p))
+        return hipErrorNotSupported;
+    const sweep_behind &bh = behind ? *behind : none;
     if constexpr (sizeof(ValueType) == 4) {
         if (p.sweep_acc_bytes == 4) {
-            launch_sweep_a<float>(p, d_x, d_y, s, warm, phase, part);
+            launch_sweep_a<float>(p, d_x, d_y, s, warm, phase, part, bh);
             return hipGetLastError();
         }
     }
-    launch_sweep_a<double>(p, d_x, d_y, s, warm, phase, part);
+    launch_sweep_a<double>(p, d_x, d_y, s, warm, phase, part, bh);
     return hipGetLastError();
 }
 

@@ -146,15 +146,17 @@ def test_distinct_plans_run_concurrently_on_two_streams(torch, dtype):
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_run_graph_overlaps_the_split_combine(torch, monkeypatch, dtype, iters):
     """A split sweep plan (rank 0 of the N = 8 cut of the 10M/160M matrix: panels cut into
-    pieces, partial sums added by k_sweep_combine) is captured as a DAG: the combine of step k
-    beside the sweep of step k + 1, two partial buffers. y after the replay (and after a second
-    replay, and a fresh x through a re-capture) matches the oracle, as with the serial capture of
-    the tools build (SPMV_GRAPH_SERIAL=1)."""
+    pieces, partial sums added by k_sweep_combine) replays with the combine of step k carried by
+    step k + 1's sweep launch (the "behind" form: extra blocks behind the units, two partial
+    buffers, a last combine kernel). y after the replay (and after a second replay, and a fresh x
+    through a re-capture) matches the oracle, as with the tools build's other capture forms
+    (SPMV_GRAPH_FORM=serial: one chain; dag: the combine on a second stream)."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     n = 10_000_000
-    for ablations in (False, True):
-        if ablations:
-            monkeypatch.setenv("SPMV_GRAPH_SERIAL", "1")
+    for ablations, env in ((False, None), (True, "SPMV_GRAPH_FORM=serial"), (True, "SPMV_GRAPH_FORM=dag")):
+        monkeypatch.delenv("SPMV_GRAPH_FORM", raising=False)
+        if env:
+            monkeypatch.setenv(*env.split("="))
         lib = spmv_hw.load(dtype, ablations=ablations)
         rp_full, _ = lib.powerlaw_row_ptr(n, 160_000_000, 65536, 4)
         b = lib.partition_rows(rp_full, 8)
@@ -172,5 +174,5 @@ def test_run_graph_overlaps_the_split_combine(torch, monkeypatch, dtype, iters):
                 plan.run_graph(x, y, iters)
                 torch.cuda.synchronize()
                 err = oracle.scaled_error(r, c, h[2], x.cpu().numpy(), ref, y.cpu().numpy())
-                assert err <= TIGHT[np.dtype(dtype)], (ablations, seed, err)
+                assert err <= TIGHT[np.dtype(dtype)], (env, seed, err)
         plan.destroy()

@@ -33,7 +33,7 @@ for s in $STEPS; do
     abmirror) run abmirror 900 python tools/ab_variants.py --workload powerlaw --dtype f32 --rounds ${AB_ROUNDS:-7} --reps 10 \
                 --variants binned#1:0,binned#1:7,binned#2:0,binned#2:7,binned#3:0,binned#3:7,binned#4:0,binned#4:7 ;;
     absteal) run absteal 900 python tools/strong_slices.py --ns ${STEAL_NS:-4,8} --slices all --variants ${STEAL_VARIANTS:-28,36,37,38} --rounds ${AB_ROUNDS:-5} --reps 20 ;;
-    abgraph) run abgraph 900 python tools/strong_slices.py --ns ${GRAPH_NS:-4,8} --slices all --graph-ab ${GRAPH_K:-20} --rounds ${AB_ROUNDS:-5} ;;
+    abgraph) run abgraph 900 python tools/strong_slices.py --ns ${GRAPH_NS:-4,8} --slices all --graph-ab ${GRAPH_K:-20} --graph-modes ${GRAPH_MODES:-product,dag,serial} --rounds ${AB_ROUNDS:-5} ;;
     tests_all) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
@@ -47,7 +47,7 @@ for s in $STEPS; do
     skew) run skew 600 python tools/skew_probe.py ${SKEW_ARGS:-} ;;
     e2e) run reader 600 python tools/bench_reader.py --dir /tmp --threads 1,8,16
          run run_elf_16m 600 ./tests/run_elf/run.elf /tmp/reader_1000000_16000000.mtx --fast-reader ;;
-    tracegraph) run trace_graph 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_graph" -o run -- python tools/strong_slices.py --ns 8 --slices ends --graph-ab 20 --rounds 1 ;;
+    tracegraph) run trace_graph 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_graph" -o run -- python tools/strong_slices.py --ns 8 --slices ends --graph-ab 20 --graph-modes ${GRAPH_MODES:-product,dag,serial} --rounds 1 ;;
     rccl1) run rccl1_strong 600 python bench.py --dist-rehearsal --scaling strong --no-weak-companion ;;
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak
               SPMV_BENCH_BACKEND=gloo run rehearse_strong 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --scaling strong ;;

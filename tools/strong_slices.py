@@ -34,9 +34,11 @@ def main():
                          "(e.g. 28,36: the split sweep with and without work stealing)")
     ap.add_argument("--rounds", type=int, default=5, help="with --variants / --graph-ab: interleaved rounds")
     ap.add_argument("--graph-ab", type=int, default=0,
-                    help="K > 0: per slice, K SpMVs replayed from one hipGraph (spmv_plan_run_graph), the "
-                         "overlapped capture of split plans against the serial one (tools build, "
-                         "SPMV_GRAPH_SERIAL=1), interleaved; ms per step")
+                    help="K > 0: per slice, K SpMVs replayed from one hipGraph (spmv_plan_run_graph) in "
+                         "each capture form of --graph-modes (tools build), interleaved; ms per step")
+    ap.add_argument("--graph-modes", default="product,dag,serial",
+                    help="with --graph-ab: the captures compared -- product (the library's choice), or "
+                         "SPMV_GRAPH_FORM=serial|dag|behind")
     a = ap.parse_args()
     dtype = np.float64 if a.dtype == "f64" else np.float32
     lib = spmv_hw.load(dtype, ablations=bool(a.graph_ab) or None)
@@ -58,14 +60,13 @@ def main():
                 plan.run(x, y)
             st = plan.stats()
             if a.graph_ab:  # overlapped vs serial graph capture, interleaved (median ms per step)
-                times = {"overlap": [], "serial": []}
+                times = {m: [] for m in a.graph_modes.split(",")}
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 for _ in range(a.rounds):
                     for mode in times:
-                        if mode == "serial":
-                            os.environ["SPMV_GRAPH_SERIAL"] = "1"
-                        else:
-                            os.environ.pop("SPMV_GRAPH_SERIAL", None)
+                        os.environ.pop("SPMV_GRAPH_FORM", None)
+                        if mode != "product":
+                            os.environ["SPMV_GRAPH_FORM"] = mode
                         plan.set_variant(28)  # drops the captured graph: the next call re-captures
                         plan.run_graph(x, y, a.graph_ab)
                         torch.cuda.synchronize()
@@ -74,12 +75,12 @@ def main():
                         ev1.record()
                         torch.cuda.synchronize()
                         times[mode].append(ev0.elapsed_time(ev1) / a.graph_ab)
-                os.environ.pop("SPMV_GRAPH_SERIAL", None)
+                os.environ.pop("SPMV_GRAPH_FORM", None)
                 med = {m: float(np.median(t)) for m, t in times.items()}
                 per[r] = {"rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "panels": st["nr_tiles"],
                           "graph_ms_per_step": {m: round(v, 5) for m, v in med.items()},
                           "graph_min_ms": {m: round(min(t), 5) for m, t in times.items()}}
-                ms = med["overlap"]
+                ms = med.get("product", min(med.values()))
                 for m in med:
                     worst_v[m] = max(worst_v.get(m, 0.0), med[m])
             elif a.variants:  # interleaved A/B of plan variants on this slice (median per variant)
