@@ -894,6 +894,10 @@ static int capture_behind(spmv_plan *p, const ValueType *d_x, ValueType *d_y, in
         bh.ccount = p->d_gcount + (k & 1);
         bh.cnext = p->d_gcount + ((k + 1) & 1);
         bh.blocks = (uint32_t)std::max(ncu, 1);
+        if (const char *v = ablation_env("SPMV_BEHIND_BLOCKS"))  // tools build: measured settings
+            bh.blocks = (uint32_t)std::max(1, atoi(v));
+        if (const char *v = ablation_env("SPMV_BEHIND_ROWS"))
+            bh.rows_per_thread = (uint32_t)std::max(1, atoi(v) / std::max(1, p->sweep_threads));
         e = launch_sweep(*p, d_x, d_y, a, false, 1, part_of(k), &bh);
     }
     if (e == hipSuccess)  // the last step's combine

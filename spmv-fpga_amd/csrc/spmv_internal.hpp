@@ -278,6 +278,7 @@ struct sweep_behind {
     uint32_t *ccount = nullptr;   // this launch's chunk counter (zero when it starts)
     uint32_t *cnext = nullptr;    // zeroed by this launch: the next launch's counter
     uint32_t blocks = 0;          // extra blocks when cpart is set
+    uint32_t rows_per_thread = 4; // a chunk is rows_per_thread x block rows (2, 4 or 8)
 };
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false,
                         int phase = 0, void *part = nullptr, const sweep_behind *behind = nullptr);

@@ -395,14 +395,14 @@ __device__ bool thief_claim_sync(SweepThief &t, unsigned long long *steal, const
 // *ccount until none is left and add the pieces' partial sums in piece order, as
 // k_sweep_combine does (the same y bit for bit). The previous step's partials (cpart) are not
 // the ones this step's units write, and the rows they store are those of split panels, which the
-// units leave to the partials.
-constexpr uint32_t kBehindRows = 4096;
-template <typename V, int T, typename A>
+// units leave to the partials. A chunk is J * T rows (J = 4 by default; the tools build's
+// SPMV_BEHIND_ROWS measures others).
+template <typename V, int T, typename A, uint32_t J>
 __device__ void combine_behind(const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ panel_unit,
                                const A *__restrict__ cpart, uint32_t stride, V *__restrict__ y,
                                uint32_t *__restrict__ ccount, uint32_t npanels)
 {
-    constexpr uint32_t J = kBehindRows / T;
+    constexpr uint32_t kBehindRows = J * T;
     const uint32_t cpp = (stride + kBehindRows - 1) / kBehindRows;  // chunks per panel
     __shared__ uint32_t claim;
     for (;;) {
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
     const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal,
     uint32_t tail16, uint32_t nunits, const A *__restrict__ cpart, uint32_t *__restrict__ ccount,
-    uint32_t *__restrict__ cnext, uint32_t npanels)
+    uint32_t *__restrict__ cnext, uint32_t npanels, uint32_t cj)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -460,7 +460,12 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     A *ylds = reinterpret_cast<A *>(smem);
     if (blockIdx.x >= nunits) {  // the previous step's combine, behind this step's units
-        combine_behind<V, T, A>(panel_row, panel_unit, cpart, stride, y, ccount, npanels);
+        if (cj == 2)
+            combine_behind<V, T, A, 2>(panel_row, panel_unit, cpart, stride, y, ccount, npanels);
+        else if (cj == 8)
+            combine_behind<V, T, A, 8>(panel_row, panel_unit, cpart, stride, y, ccount, npanels);
+        else
+            combine_behind<V, T, A, 4>(panel_row, panel_unit, cpart, stride, y, ccount, npanels);
         return;
     }
     if (cnext && blockIdx.x == 0 && threadIdx.x == 0)  // the next launch's claim counter
@@ -1188,13 +1193,13 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr, \
-                       (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u)
+                       (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, 0u)
     // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
 #define PKD(ST, TAIL)                                                                                 \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, gridb, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr, (uint32_t)(TAIL), \
-                       (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels)
+                       (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels, bh.rows_per_thread)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)

@@ -38,7 +38,7 @@ def main():
                          "each capture form of --graph-modes (tools build), interleaved; ms per step")
     ap.add_argument("--graph-modes", default="product,dag,serial",
                     help="with --graph-ab: the captures compared -- product (the library's choice), or "
-                         "SPMV_GRAPH_FORM=serial|dag|behind")
+                         "SPMV_GRAPH_FORM=serial|dag|behind, with _rN (SPMV_BEHIND_ROWS) / _bN (SPMV_BEHIND_BLOCKS)")
     a = ap.parse_args()
     dtype = np.float64 if a.dtype == "f64" else np.float32
     lib = spmv_hw.load(dtype, ablations=bool(a.graph_ab) or None)
@@ -64,9 +64,13 @@ def main():
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 for _ in range(a.rounds):
                     for mode in times:
-                        os.environ.pop("SPMV_GRAPH_FORM", None)
-                        if mode != "product":
-                            os.environ["SPMV_GRAPH_FORM"] = mode
+                        for k in ("SPMV_GRAPH_FORM", "SPMV_BEHIND_ROWS", "SPMV_BEHIND_BLOCKS"):
+                            os.environ.pop(k, None)
+                        form, *knobs = mode.split("_")  # e.g. behind_r2048_b512
+                        if form != "product":
+                            os.environ["SPMV_GRAPH_FORM"] = form
+                        for kn in knobs:
+                            os.environ["SPMV_BEHIND_ROWS" if kn[0] == "r" else "SPMV_BEHIND_BLOCKS"] = kn[1:]
                         plan.set_variant(28)  # drops the captured graph: the next call re-captures
                         plan.run_graph(x, y, a.graph_ab)
                         torch.cuda.synchronize()
@@ -75,7 +79,8 @@ def main():
                         ev1.record()
                         torch.cuda.synchronize()
                         times[mode].append(ev0.elapsed_time(ev1) / a.graph_ab)
-                os.environ.pop("SPMV_GRAPH_FORM", None)
+                for k in ("SPMV_GRAPH_FORM", "SPMV_BEHIND_ROWS", "SPMV_BEHIND_BLOCKS"):
+                    os.environ.pop(k, None)
                 med = {m: float(np.median(t)) for m, t in times.items()}
                 per[r] = {"rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "panels": st["nr_tiles"],
                           "graph_ms_per_step": {m: round(v, 5) for m, v in med.items()},
