@@ -8,8 +8,10 @@ x and y resident in HBM before the timed region. The K timed steps are replayed 
 (spmv_plan_run_graph, captured and warmed before the timed region); the same K steps with one
 host launch each are timed first (graph.eager_ms_per_step), and their HIP-event kernel times give
 the roofline. For a split plan (the N >= 4 strong-scaling slices: panels cut into pieces whose
-partial sums a second kernel adds) the graph runs the combine of step k beside the sweep of step
-k + 1; every step still computes all of y.
+partial sums a second kernel adds) the graph carries the combine of step k as extra blocks of step
+k + 1's sweep launch, which run in that sweep's tail, and one combine kernel after the last step
+(DESIGN.md §6): every step still computes all of y, but a step's time can then fall below the
+eager sweep + combine time of one SpMV.
 
 Workloads:
   powerlaw (default, config 3): n = m = 10,000,000, nnz = 160,000,000, Pareto(2) row lengths
