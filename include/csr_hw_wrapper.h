@@ -130,7 +130,11 @@ int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, v
 /* Iterative / persistent mode: `iters` consecutive SpMVs d_y = A * d_x, captured once into a
  * hipGraph (re-captured when d_x, d_y or iters change) and replayed on `stream` per call, so
  * back-to-back SpMVs pay no per-launch host cost. With timing on, one event pair brackets the
- * whole graph (spmv_plan_get_timing then reports ms per graph). */
+ * whole graph (spmv_plan_get_timing then reports ms per graph). The SpMVs of one replay are
+ * independent (same x), so a split sweep plan pipelines them: step k's partial sums are added by
+ * extra blocks of step k + 1's sweep launch, and a last combine kernel ends the graph (the first
+ * capture allocates a second partial-sum buffer for this). d_y is complete when the graph
+ * has run. */
 int spmv_plan_run_graph(spmv_plan *plan, const ValueType *d_x, ValueType *d_y, int iters, void *stream);
 int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
 /* Kernel variants (performance experiments; every variant computes the same y).
