@@ -176,3 +176,34 @@ def test_run_graph_overlaps_the_split_combine(torch, monkeypatch, dtype, iters):
                 err = oracle.scaled_error(r, c, h[2], x.cpu().numpy(), ref, y.cpu().numpy())
                 assert err <= TIGHT[np.dtype(dtype)], (env, seed, err)
         plan.destroy()
+
+
+@pytest.mark.parametrize("iters", [2, 5])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_run_graph_behind_two_pieces(torch, monkeypatch, dtype, iters):
+    """The behind form on a panel cut into two pieces (rank 1 of the N = 4 cut: ~126 panels x 2),
+    an odd step count (the last combine reads the second partial buffer), then eager runs of the
+    same plan after the replay (the launch's extra blocks and counters leave nothing behind)."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    n = 10_000_000
+    lib = spmv_hw.load(dtype)
+    rp_full, _ = lib.powerlaw_row_ptr(n, 160_000_000, 65536, 4)
+    b = lib.partition_rows(rp_full, 4)
+    r0, r1 = int(b[1]), int(b[2])
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 160_000_000, seed=4, row_begin=r0, row_end=r1)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    assert plan.stats()["nr_tiles"] > 200
+    h = _host(rp, col, val)
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    x = spmv_hw.gen_vector(lib, n, seed=9, lo=-1.0)
+    ref = (oracle.spmv_fp64acc if dtype == np.float32 else oracle.spmv_gold)(r, c, h[2], x.cpu().numpy())
+    for run in ("graph", "graph", "eager"):
+        y = torch.full((r1 - r0,), float("nan"), dtype=x.dtype, device="cuda")
+        if run == "graph":
+            plan.run_graph(x, y, iters)
+        else:
+            plan.run(x, y)
+        torch.cuda.synchronize()
+        err = oracle.scaled_error(r, c, h[2], x.cpu().numpy(), ref, y.cpu().numpy())
+        assert err <= TIGHT[np.dtype(dtype)], (run, err)
+    plan.destroy()
