@@ -793,8 +793,9 @@ int spmv_plan_run(const spmv_plan *cp, const ValueType *d_x, ValueType *d_y, voi
     return run_impl(p, d_x, d_y, (hipStream_t)stream, p->timing);
 }
 
-// A split sweep plan (panels cut into pieces whose partial sums k_sweep_combine adds) is captured
-// as a DAG instead of a chain: the combine of step k runs on a second capture stream beside the
+// The "dag" form, for split plans whose sweep launch cannot carry the combine (the behind form
+// below measured faster; SPMV_GRAPH_FORM=dag forces this one in the tools build): the combine
+// of step k runs on a second capture stream beside the
 // sweep of step k + 1, the steps' partial sums alternate between two buffers, and the sweep of
 // step k + 2 waits for the combine of step k (its buffer). The combine needs no LDS, so its
 // workgroups fit beside the sweep's one 1024-thread workgroup per CU. Every step still computes

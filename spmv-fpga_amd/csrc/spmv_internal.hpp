@@ -137,7 +137,8 @@ struct spmv_plan {
     uint32_t *d_panel_unit = nullptr;  // first unit of each panel [npanels + 1]
     void *d_part = nullptr;            // split > 1: nunits x (panel_rmax + 1) partial sums (accumulator type)
     std::vector<void *> gpart;         // spmv_plan_run_graph: a second partial buffer beside d_part, so
-                                       // that the combine of step k runs beside the sweep of step k + 1
+                                       // that step k + 1's sweep can run while step k's partials wait
+                                       // for their combine
     uint32_t *d_gcount = nullptr;      // spmv_plan_run_graph, "behind" form: two chunk counters
     unsigned long long *d_steal = nullptr;  // tools build, split > 1: per unit, iterations claimed
                                             // from the front (low word) and back (high word) by the
@@ -204,7 +205,7 @@ struct spmv_plan {
     // spmv_plan_run_graph: `giters` SpMVs on (gx, gy) captured once, replayed per call
     hipGraphExec_t gexec = nullptr;
     hipStream_t gstream = nullptr;
-    hipStream_t gstream2 = nullptr;  // second capture stream (split sweep: the combines)
+    hipStream_t gstream2 = nullptr;  // second capture stream (the tools build's "dag" form: the combines)
     const ValueType *gx = nullptr;
     ValueType *gy = nullptr;
     int giters = 0;
