@@ -77,8 +77,34 @@ def timeline(lib, plan, x, y, units):
             "per_xcc": per_xcc}
 
 
+def consistency(lib, plan, x, y, units, launches):
+    """Is a unit's sweep time a property of the unit? Per-unit sweep durations over `launches`
+    launches: the correlation of two launches' durations, the spread of the per-unit means (the
+    part a one-time re-cut of the units could remove) and of the residuals (the part it could
+    not), and the longest sweep if every unit's mean were brought to the median."""
+    durs = []
+    for _ in range(launches):
+        plan.run(x, y)
+        torch.cuda.synchronize()
+        a = read_stamps(lib, units)
+        t = a[:, :2].astype(np.int64)
+        durs.append((t[:, 1] - t[:, 0]) / 100.0)
+    d = np.array(durs)  # launches x units
+    mean = d.mean(axis=0)
+    resid = d - mean
+    cc = [float(np.corrcoef(d[i], d[i + 1])[0, 1]) for i in range(launches - 1)]
+    med = float(np.median(mean))
+    return {"launches": launches, "corr_consecutive_p50": round(float(np.median(cc)), 3),
+            "unit_mean_us": {"min": pct(mean, 0), "p50": pct(mean, 50), "max": pct(mean, 100)},
+            "resid_us": {"p5": pct(resid, 5), "p95": pct(resid, 95), "max": pct(resid, 100)},
+            "max_sweep_us_p50": round(float(np.median(d.max(axis=1))), 2),
+            "max_sweep_us_if_rebalanced_p50": round(float(np.median((med + resid).max(axis=1))), 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--consistency", type=int, default=0,
+                    help="K > 1: per-unit sweep durations over K launches (is the tail systematic?)")
     ap.add_argument("--slices", default="0/8,0/4,0/1", help="k/N: rows of slice k of N (nnz-balanced)")
     ap.add_argument("--binned", action="store_true",
                     help="the fp32 10M/160M matrix on the binned kernel instead: both passes' timelines")
@@ -117,6 +143,8 @@ def main():
         out = {"slice": sl, "rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "format": st["format"]}
         if st["kernel"] == 2:
             out.update(timeline(lib, plan, x, y, st["nr_tiles"]))
+            if a.consistency > 1:
+                out["consistency"] = consistency(lib, plan, x, y, st["nr_tiles"], a.consistency)
         print(json.dumps(out), flush=True)
         plan.destroy()
         del rp, col, val, y
