@@ -793,7 +793,10 @@ def main():
     barrier(world)
     ms = spmv_dist.max_over_ranks((time.perf_counter() - tg0) * 1e3 / args.steps, dev)
     graph = {"iters": args.steps, "ms_per_step": round(ms, 5), "timed": "headline (value, ms_per_step)",
-             "eager_ms_per_step": round(eager_ms, 5)}
+             "eager_ms_per_step": round(eager_ms, 5),
+             # how the replay orders the steps (plan stats format bits 8 / 9)
+             "form": ("behind: each step's combine in the next step's sweep launch" if st["format"] & 256 else
+                      "dag: the combines on a second stream" if st["format"] & 512 else "serial")}
 
     xtiles = det = binned = None
     if want_xtiles:  # reported beside the headline, never fatal to it

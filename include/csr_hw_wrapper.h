@@ -109,7 +109,10 @@ typedef struct spmv_plan_stats {
                                     sorted segments with 1-byte row deltas (kernel 6); bit 6:
                                     delta-coded columns, 11-byte fp64 / 7-byte fp32 sweep entries
                                     (kernel 2); bit 7: the tools library's work-stealing
-                                    variants 37-39 are selected (kernel 2, split plans) */
+                                    variants 37-39 are selected (kernel 2, split plans); bit 8:
+                                    spmv_plan_run_graph pipelines the steps, each step's combine
+                                    behind the next sweep launch; bit 9: the same with the
+                                    combines on a second stream (split plans, 2+ steps) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are

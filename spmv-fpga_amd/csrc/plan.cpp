@@ -1027,7 +1027,8 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
                  (p->tile_col_bytes == 1 ? 8 : 0) | (p->tile_clustered ? 16 : 0) |
                  (p->kernel == kKernelBinned && p->b_delta ? 32 : 0) |
                  (p->kernel == kKernelSweep && p->sweep_steal &&
-                          (p->sweep_variant == 37 || p->sweep_variant == 38 || p->sweep_variant == 39) ? 128 : 0);
+                          (p->sweep_variant == 37 || p->sweep_variant == 38 || p->sweep_variant == 39) ? 128 : 0) |
+                 (graph_form(p) == 2 ? 256 : graph_form(p) == 1 ? 512 : 0);
     return 0;
 }
 

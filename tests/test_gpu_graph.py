@@ -164,6 +164,8 @@ def test_run_graph_overlaps_the_split_combine(torch, monkeypatch, dtype, iters):
         rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 160_000_000, seed=4, row_begin=r0, row_end=r1)
         plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
         assert plan.stats()["nr_tiles"] > 200  # split: ~62 panels in ~4 pieces each
+        form = plan.stats()["format"] & (256 | 512)  # the capture form run_graph will use
+        assert form == {None: 256, "SPMV_GRAPH_FORM=serial": 0, "SPMV_GRAPH_FORM=dag": 512}[env], (env, form)
         h = _host(rp, col, val)
         r, c = h[0].view(np.uint32), h[1].view(np.uint32)
         for seed in (6, 7):  # a new x buffer re-captures the graph
