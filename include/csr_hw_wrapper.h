@@ -112,7 +112,10 @@ typedef struct spmv_plan_stats {
                                     variants 37-39 are selected (kernel 2, split plans); bit 8:
                                     spmv_plan_run_graph pipelines the steps, each step's combine
                                     behind the next sweep launch; bit 9: the same with the
-                                    combines on a second stream (split plans, 2+ steps) */
+                                    combines on a second stream (split plans, 2+ steps);
+                                    bits 10 / 11: the pieces of a split sweep plan are cut with
+                                    the even / the odd XCCs' units lighter (the cut the build
+                                    timed fastest on this GPU, or env SPMV_SWEEP_XCC_BIAS) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are

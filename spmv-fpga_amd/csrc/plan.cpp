@@ -402,6 +402,8 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
     // failure here only means the first run loads them)
     if (P.kernel == kKernelSweep) {
         (void)launch_sweep(P, nullptr, nullptr, s, true);
+        if (sweep_tune_bias(P, s))
+            return 1;
     } else if (P.kernel == kKernelBinned) {
         (void)launch_binned(P, nullptr, nullptr, s, true);
     } else if (P.kernel == kKernelBlocked) {
@@ -1028,7 +1030,9 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
                  (p->kernel == kKernelBinned && p->b_delta ? 32 : 0) |
                  (p->kernel == kKernelSweep && p->sweep_steal &&
                           (p->sweep_variant == 37 || p->sweep_variant == 38 || p->sweep_variant == 39) ? 128 : 0) |
-                 (graph_form(p) == 2 ? 256 : graph_form(p) == 1 ? 512 : 0);
+                 (graph_form(p) == 2 ? 256 : graph_form(p) == 1 ? 512 : 0) |
+                 (p->kernel == kKernelSweep && p->sweep_split > 1 && p->xbias_split > 0.0 ? 1024 : 0) |
+                 (p->kernel == kKernelSweep && p->sweep_split > 1 && p->xbias_split < 0.0 ? 2048 : 0);
     return 0;
 }
 

@@ -1322,6 +1322,96 @@ hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y
     return hipGetLastError();
 }
 
+// The pieces of every panel: whole chunks, cut with the even / odd XCC bias d (the weight of
+// units [0, u) is u - d (u & 1): the units block-round-robin dispatch sends to even XCCs get
+// (1 - d) x the mean, the odd ones (1 + d) x); d = 0 cuts evenly
+static void cut_units(const std::vector<uint32_t> &poff, const std::vector<uint32_t> &punit, double d,
+                      std::vector<uint32_t> &uent)
+{
+    const uint32_t P = (uint32_t)punit.size() - 1, U = punit[P];
+    uent.assign((size_t)U + 1, 0);
+    auto wc = [&](uint32_t u) { return double(u) - d * double(u & 1); };
+    for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
+        const uint32_t k = punit[q + 1] - punit[q], u0 = punit[q];
+        for (uint32_t t = 0; t < k; ++t) {
+            const uint64_t c = d != 0.0 ? (uint64_t)(double(chunks) * (wc(u0 + t) - wc(u0)) / (wc(u0 + k) - wc(u0)))
+                                        : chunks * t / k;
+            uent[u0 + t] = (uint32_t)(poff[q] + kSweepChunk * c);
+        }
+    }
+    uent[U] = poff[P];
+}
+
+// Split plans: which XCCs sweep slower is a property of the GPU, not of the matrix (even ones on
+// the boxes of round 3, odd ones on some of round 4: DESIGN.md §6), and the pieces' cut is cheap
+// to redo (unit_ent only). So the build times three cuts of the pieces -- even XCCs lighter by
+// 2 %, even, odd lighter by 2 % -- interleaved (3 rounds of 3 SpMVs each, on scratch x / y)
+// and keeps the fastest. A few ms per plan.
+int sweep_tune_bias(spmv_plan &p, hipStream_t s)
+{
+    if (!p.xbias_tune || p.sweep_det)
+        return 0;
+    const double cand[3] = {0.02, 0.0, -0.02};
+    ValueType *x = nullptr, *y = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::vector<uint32_t> uent;
+    float best = -1.0f, t[3][3] = {};
+    int pick = 0;
+    hipError_t err = hipMalloc((void **)&x, std::max<uint64_t>(p.nr_cols, 1) * sizeof(ValueType));
+    if (err == hipSuccess)
+        err = hipMalloc((void **)&y, std::max<uint64_t>(p.nr_rows, 1) * sizeof(ValueType));
+    if (err == hipSuccess)
+        err = hipMemsetAsync(x, 0, std::max<uint64_t>(p.nr_cols, 1) * sizeof(ValueType), s);
+    if (err == hipSuccess)
+        err = hipEventCreate(&e0);
+    if (err == hipSuccess)
+        err = hipEventCreate(&e1);
+    for (int r = 0; r < 3 && err == hipSuccess; ++r)
+        for (int c = 0; c < 3 && err == hipSuccess; ++c) {
+            cut_units(p.h_poff, p.h_punit, cand[c], uent);
+            err = hipMemcpy(p.d_unit_ent, uent.data(), uent.size() * 4, hipMemcpyHostToDevice);
+            if (err == hipSuccess)
+                err = launch_sweep(p, x, y, s);  // warm this cut
+            if (err == hipSuccess)
+                err = hipEventRecord(e0, s);
+            for (int k = 0; k < 3 && err == hipSuccess; ++k)
+                err = launch_sweep(p, x, y, s);
+            if (err == hipSuccess)
+                err = hipEventRecord(e1, s);
+            if (err == hipSuccess)
+                err = hipEventSynchronize(e1);
+            if (err == hipSuccess)
+                err = hipEventElapsedTime(&t[c][r], e0, e1);
+        }
+    if (err == hipSuccess) {
+        for (int c = 0; c < 3; ++c) {
+            float m[3] = {t[c][0], t[c][1], t[c][2]};
+            std::sort(m, m + 3);
+            if (best < 0.0f || m[1] < best)
+                best = m[1], pick = c;
+        }
+        cut_units(p.h_poff, p.h_punit, cand[pick], uent);
+        err = hipMemcpy(p.d_unit_ent, uent.data(), uent.size() * 4, hipMemcpyHostToDevice);
+        p.xbias_split = cand[pick];
+    }
+    if (e0)
+        (void)hipEventDestroy(e0);
+    if (e1)
+        (void)hipEventDestroy(e1);
+    if (x)
+        (void)hipFree(x);
+    if (y)
+        (void)hipFree(y);
+    p.h_poff.clear();
+    p.h_punit.clear();
+    if (err != hipSuccess) {
+        set_error(std::string("build_sweep: bias tuning: ") + hipGetErrorString(err));
+        return 1;
+    }
+    return 0;
+}
+
 // Host: panel boundaries (nnz-balanced, <= rmax rows each), then the device sort + scatter.
 // Work units: when the slice has at least one panel per resident workgroup, panels are rounded
 // to whole rounds of workgroups and each panel is one unit. When it has fewer (a slice of fewer
@@ -1461,22 +1551,19 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     const uint32_t U = punit[P];
     std::vector<uint32_t> uent, upanel(std::max<uint32_t>(U, 1));
     bool multi = false;
-    uent.assign((size_t)U + 1, 0);
     for (uint32_t q = 0; q < P; ++q) {
-        const uint64_t chunks = (uint64_t(poff[q + 1]) - poff[q]) / kSweepChunk;
-        const uint32_t k = punit[q + 1] - punit[q];
-        multi |= k > 1;
-        const uint32_t u0 = punit[q];
-        auto wc = [&](uint32_t u) { return double(u) - xbias * double(u & 1); };  // weight of units [0, u)
-        for (uint32_t t = 0; t < k; ++t) {
-            const uint64_t c = split_mode && xbias != 0.0
-                                   ? (uint64_t)(double(chunks) * (wc(u0 + t) - wc(u0)) / (wc(u0 + k) - wc(u0)))
-                                   : chunks * t / k;
-            uent[u0 + t] = (uint32_t)(poff[q] + kSweepChunk * c);
-            upanel[u0 + t] = q;
-        }
+        multi |= punit[q + 1] - punit[q] > 1;
+        for (uint32_t u = punit[q]; u < punit[q + 1]; ++u)
+            upanel[u] = q;
     }
-    uent[U] = poff[P];
+    cut_units(poff, punit, split_mode ? xbias : 0.0, uent);
+    p.xbias_split = split_mode ? xbias : 0.0;
+    // a split plan on a whole chip whose bias no env pins: sweep_tune_bias picks it on this GPU
+    p.xbias_tune = split_mode && multi && !xbenv && chip_cus == 256 && !det;
+    if (p.xbias_tune) {
+        p.h_poff = poff;
+        p.h_punit = punit;
+    }
     p.sweep_split = multi ? std::max<uint32_t>(split, 2) : 1;  // > 1: combine kernel needed
     p.nunits = U;
     if (multi) {

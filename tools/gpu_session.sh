@@ -51,7 +51,8 @@ for s in $STEPS; do
     wgcons) run wgcons 600 python tools/wg_timeline.py --slices ${WG_SLICES:-0/8,7/8,0/4,0/1} --consistency ${WG_K:-20} ;;
     abbias) for i in 1 2 3; do
               SPMV_SWEEP_XCC_BIAS=0 run abbias0_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_0
-              run abbiasd_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_default
+              SPMV_SWEEP_XCC_BIAS=0.02 run abbiasd_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_0.02
+              run abbiast_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_tuned
             done ;;
     rccl1) run rccl1_strong 600 python bench.py --dist-rehearsal --scaling strong --no-weak-companion ;;
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak

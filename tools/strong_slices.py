@@ -83,6 +83,7 @@ def main():
                     os.environ.pop(k, None)
                 med = {m: float(np.median(t)) for m, t in times.items()}
                 per[r] = {"rows": r1 - r0, "nnz": st["nr_nzeros"], "kernel": st["kernel"], "panels": st["nr_tiles"],
+                          "xcc_lighter": "even" if st["format"] & 1024 else "odd" if st["format"] & 2048 else "none",
                           "graph_ms_per_step": {m: round(v, 5) for m, v in med.items()},
                           "graph_min_ms": {m: round(min(t), 5) for m, t in times.items()}}
                 ms = med.get("product", min(med.values()))
