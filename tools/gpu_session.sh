@@ -49,7 +49,7 @@ for s in $STEPS; do
          run run_elf_16m 600 ./tests/run_elf/run.elf /tmp/reader_1000000_16000000.mtx --fast-reader ;;
     tracegraph) run trace_graph 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_graph" -o run -- python tools/strong_slices.py --ns 8 --slices ends --graph-ab 20 --graph-modes ${GRAPH_MODES:-product,dag,serial} --rounds 1 ;;
     wgcons) run wgcons 600 python tools/wg_timeline.py --slices ${WG_SLICES:-0/8,7/8,0/4,0/1} --consistency ${WG_K:-20} ;;
-    abbias) for i in 1 2 3; do
+    abbias) for i in $(seq 1 ${AB_ITERS:-3}); do
               SPMV_SWEEP_XCC_BIAS=0 run abbias0_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_0
               SPMV_SWEEP_XCC_BIAS=0.02 run abbiasd_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_0.02
               run abbiast_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_tuned
