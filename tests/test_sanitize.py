@@ -12,6 +12,7 @@ small driver (tests/sanitize/host_check.cpp). This suite builds them and runs:
     defects SURVEY B2/B3 found in the reference's reader and accumulation (csr.cpp:115-126,
     csr_hw.cpp:1549-1553).
 CPU only; no GPU, no HIP."""
+import fcntl
 import os
 import shutil
 import subprocess
@@ -35,7 +36,12 @@ ENV = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:halt_on_error=1:verify_a
 def built():
     if not shutil.which("g++"):
         pytest.skip("g++ not available")
-    subprocess.run(["make", "-s", "-j3", "-C", SAN], check=True, timeout=600)
+    # one build at a time: pytest-xdist workers that each run this module's fixture must not
+    # relink a binary another worker is running
+    os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-j3", "-C", SAN], check=True, timeout=600)
     return {k: os.path.join(BUILD, f"host_check_{k}") for k in BINS}
 
 
