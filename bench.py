@@ -79,7 +79,8 @@ def parse(argv=None):
                          "line is printed without them")
     ap.add_argument("--extras-timeout-status", type=int, default=0,
                     help="exit status after the watchdog printed the line (the line stays valid: it "
-                         "carries `extras_timeout`; set e.g. 3 to make a hang visible to an exit-code check)")
+                         "carries `extras_timeout`, and at N > 1 its parity already passed; set e.g. 3 to "
+                         "make a hang visible to an exit-code check)")
     ap.add_argument("--no-det", action="store_true",
                     help="skip the deterministic-sweep side line (SPMV_SWEEP_DETERMINISTIC=1)")
     ap.add_argument("--no-xtiles", action="store_true",
@@ -102,7 +103,13 @@ def parse(argv=None):
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
     ap.add_argument("--spawn-grace", type=float, default=60.0,
-                    help="self-launch: seconds the other ranks may run on after one rank failed")
+                    help="self-launch: seconds the other ranks may run on after one rank exited (with any "
+                         "status); ranks still running then are hung, killed, and the run fails")
+    ap.add_argument("--run-timeout", type=float, default=900.0,
+                    help="seconds the whole run may take (below the driver's limit): then every rank is "
+                         "killed and one JSON error line names each rank's last stage; exit status 124")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="N > 1: timeout of every torch.distributed collective (init_process_group)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="every rank prints its launch environment as JSON and exits before any GPU call")
     ap.add_argument("--dry-launch-rc", default="",
@@ -135,34 +142,106 @@ def _status(rc):
     return 128 - rc if rc is not None and rc < 0 else (rc or 0)
 
 
+STAGE_FD_ENV = "SPMV_BENCH_STAGE_FD"
+
+
+def _die_with_parent():
+    """preexec of a self-launched rank: SIGKILL when the parent dies (Linux prctl
+    PR_SET_PDEATHSIG), so a killed parent leaves no rank behind on the GPU."""
+    try:
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGKILL, 0, 0, 0)
+    except Exception:
+        pass
+
+
+def error_line(args, error, stages, rc):
+    """The one JSON line of a run that produced no measurement: what failed and each rank's last
+    stage (init, build, warmup, timed, parity, extras, emitted)."""
+    return json.dumps({"metric": "SpMV GFLOP/s + effective HBM GB/s (% roofline), fp64, 1/2/4/8 MI355X",
+                       "value": None, "unit": "GFLOP/s", "n_gpus": args.gpus, "error": error, "rc": rc,
+                       "stage": {str(r): st for r, st in sorted(stages.items())}})
+
+
 def spawn_ranks(args, argv):
+    """Starts the N ranks and supervises them (csr_hw_wrapper.cpp:193-288 is
+    synchronous and always reports). Every rank writes "rank:stage" lines into one pipe. The
+    parent kills every rank and fails (status 124) when --run-timeout expires; once any rank has
+    exited, the others get --spawn-grace seconds, then they are killed as hung. When rank 0 never
+    printed its line, the parent prints one JSON error line with each rank's last stage."""
     n = args.gpus
     port = _free_port()
+    r_fd, w_fd = os.pipe()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPMV_BENCH_LAUNCHER="bench.py")
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPMV_BENCH_LAUNCHER="bench.py",
+                   **{STAGE_FD_ENV: str(w_fd)})
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
-                                      stdout=None if r == 0 else sys.stderr))
+                                      stdout=None if r == 0 else sys.stderr, pass_fds=(w_fd,),
+                                      preexec_fn=_die_with_parent))
+    os.close(w_fd)
+    os.set_blocking(r_fd, False)
 
-    def stop(signum, _frame):  # the parent is being stopped: take the workers with it
+    def kill_all():
         for p in procs:
             if p.poll() is None:
-                p.terminate()
+                p.kill()
+        for p in procs:
+            p.wait()
+
+    def stop(signum, _frame):  # the parent is being stopped: take the workers with it
+        kill_all()
         sys.exit(128 + signum)
 
     for sig in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sig, stop)
-    failed_at = None
+    stages = {r: "launched" for r in range(n)}
+    pending = b""
+
+    def read_stages():
+        nonlocal pending
+        while True:
+            try:
+                chunk = os.read(r_fd, 65536)
+            except BlockingIOError:
+                return
+            if not chunk:
+                return
+            pending += chunk
+            *lines, pending = pending.split(b"\n")
+            for ln in lines:
+                rank, _, st = ln.decode(errors="replace").partition(":")
+                if rank.isdigit() and int(rank) in stages:
+                    stages[int(rank)] = st
+
+    t0 = time.monotonic()
+    first_exit, error = None, None
     while any(p.poll() is None for p in procs):
-        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
-            failed_at = time.monotonic()
-        if failed_at is not None and time.monotonic() - failed_at > args.spawn_grace:
-            for p in procs:  # a rank died: the others may wait in a collective forever
-                if p.poll() is None:
-                    p.kill()
+        read_stages()
+        now = time.monotonic()
+        if first_exit is None and any(p.poll() is not None for p in procs):
+            first_exit = now
+        if now - t0 > args.run_timeout:
+            error = f"run timeout: ranks still running after {args.run_timeout:g} s, all killed"
+            kill_all()
+            break
+        if first_exit is not None and now - first_exit > args.spawn_grace:
+            hung = [r for r, p in enumerate(procs) if p.poll() is None]
+            error = f"ranks {hung} still running {args.spawn_grace:g} s after another rank exited, killed as hung"
+            kill_all()
+            break
         time.sleep(0.2)
-    return max(_status(p.returncode) for p in procs)
+    read_stages()
+    os.close(r_fd)
+    rc = 124 if error and error.startswith("run timeout") else max(_status(p.returncode) for p in procs)
+    if error or rc != 0:
+        if stages.get(0) != "emitted":
+            print(error_line(args, error or f"rank exit statuses {[_status(p.returncode) for p in procs]}",
+                             stages, rc), flush=True)
+        print(f"bench.py: {error or 'a rank failed'}; stages {stages}", file=sys.stderr, flush=True)
+        rc = rc or 1
+    return rc
 
 
 def dry_launch(args):
@@ -173,11 +252,50 @@ def dry_launch(args):
     print(json.dumps({"dry_launch": True, "gpus": args.gpus, "pid": os.getpid(), **env}), flush=True)
     codes = dict(kv.split(":") for kv in args.dry_launch_rc.split(",") if kv)
     code = codes.get(str(rank), "0")
+    stage("init")
     if code == "hang":
+        stage("timed")  # a rank stuck where a collective would hold it
         time.sleep(3600)
+    if code == "0":
+        stage("emitted" if rank == 0 else "done")
     if int(code) < 0:
         os.kill(os.getpid(), -int(code))
     return int(code)
+
+
+_STAGE = ["start"]
+
+
+def stage(name):
+    """This rank's progress: kept for the run watchdog's error line and, under the self-launch
+    parent, written to its pipe as "rank:stage"."""
+    _STAGE[0] = name
+    fd = os.environ.get(STAGE_FD_ENV)
+    if fd:
+        try:
+            os.write(int(fd), f"{os.environ.get('RANK', '0')}:{name}\n".encode())
+        except (OSError, ValueError):
+            pass
+
+
+def arm_run_watchdog(args):
+    """Without the self-launch parent (N = 1, or ranks started by torch.distributed.run): the
+    run's own deadline. After --run-timeout seconds rank 0 prints one JSON error line with its
+    stage and every rank exits 124 -- a hang (rendezvous, barrier, a collective, a kernel that
+    never ends) costs minutes, not the driver's whole limit."""
+    if os.environ.get("SPMV_BENCH_LAUNCHER") == "bench.py":
+        return None  # the parent supervises (spawn_ranks)
+
+    def expire():
+        if int(os.environ.get("RANK", "0")) == 0 and _STAGE[0] != "emitted":
+            print(error_line(args, f"run timeout after {args.run_timeout:g} s", {0: _STAGE[0]}, 124), flush=True)
+        sys.stdout.flush()
+        os._exit(124)
+
+    t = threading.Timer(args.run_timeout, expire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 if __name__ == "__main__":
@@ -185,6 +303,7 @@ if __name__ == "__main__":
     if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(_args, sys.argv[1:]))
     if _args.dry_launch:
+        arm_run_watchdog(_args)
         sys.exit(dry_launch(_args))
 
 import torch  # noqa: E402
@@ -214,10 +333,15 @@ def setup_dist(args):
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
     if args.multi:
+        import datetime
+        # every collective (rendezvous, barriers, max-over-ranks, the exchange) gives up after
+        # --collective-timeout instead of waiting forever for a rank that is gone or stuck
+        tmo = datetime.timedelta(seconds=args.collective_timeout)
+        stage("init")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     return world, rank, dev_index
 
 
@@ -689,7 +813,7 @@ def strong_companion(lib, args, world, rank, dev, stream):
     return res
 
 
-def distributed_parity(lib, args, world, rank, dev, y, st):
+def distributed_parity(lib, args, world, rank, dev, y, st, held=None):
     """N > 1: the reference checks every spmv_hw result (main.cpp:77-82); so does this line.
     Strong scaling (config 4): every rank's y slice is gathered on rank 0 (spmv_dist.exchange_gather)
     and the assembled 10M-row y is checked against the oracle's spmv_gold of the whole matrix,
@@ -713,6 +837,8 @@ def distributed_parity(lib, args, world, rank, dev, y, st):
         cnt[rank] = float(st["nr_rows"])
         counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
         y_full = spmv_dist.exchange_gather(y, counts)
+        if held is not None:
+            held["y_full"] = y_full  # rank 0: the assembled y (the dependent form's check)
         res = {"scope": f"y of all {world} row slices gathered on rank 0 vs spmv_gold of the whole matrix",
                "rows_checked": int(counts.sum())}
         if rank == 0:
@@ -737,8 +863,73 @@ def distributed_parity(lib, args, world, rank, dev, y, st):
     return res
 
 
+def serial_chain_ms(plan, x, y, steps, world, dev):
+    """The K steps as a serial chain: K spmv_plan_run calls captured into one graph by the
+    caller (torch.cuda.graph), so every step -- a split plan's sweep and its combine -- ends
+    before the next begins, as one spmv_hw call is one complete SpMV (csr_hw_wrapper.cpp:200-285).
+    Replayed once untimed, then timed; max over ranks."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(steps):
+            plan.run(x, y)
+    g.replay()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    barrier(world)
+    ms = spmv_dist.max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, dev)
+    del g
+    return ms
+
+
+def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full):
+    """The dependent form (x <- A x): every step is this rank's SpMV into its
+    slice and the all-gather of the slices into every rank's next x (spmv_dist.exchange_allgather),
+    so step k + 1 cannot start before step k's exchange has ended. Timed over K steps from the
+    headline's x, max over ranks. Checked: one step from that x gives, on every rank, the y the
+    parity gather assembled on rank 0 (within 1e-12 relative: the LDS adds' order)."""
+    cnt = [0.0] * world
+    cnt[rank] = float(st["nr_rows"])
+    counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
+    nloc = int(st["nr_rows"])
+    ys = torch.empty(nloc, dtype=y.dtype, device=dev)
+    bufs = [x.clone(), torch.empty_like(x)]
+
+    def step(k):
+        src, dst = bufs[k % 2], bufs[(k + 1) % 2]
+        plan.run(src, ys)
+        spmv_dist.exchange_allgather(ys, counts, out=dst)
+
+    step(0)  # warm (communicator, staging buffers)
+    bufs[0].copy_(x)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    torch.cuda.synchronize()
+    barrier(world)
+    ms = spmv_dist.max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, dev)
+    bufs[0].copy_(x)
+    step(0)  # x1 = A x on every rank
+    torch.cuda.synchronize()
+    diff = 0.0
+    if rank == 0 and y_full is not None:
+        ref = y_full.to(dev).double()
+        diff = float(((bufs[1].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-300)).item())
+    diff = spmv_dist.max_over_ranks(diff, dev)
+    del bufs, ys
+    return {"ms_per_step": round(ms, 5), "steps": steps,
+            "form": "SpMV into the rank's slice, then all-gather of the slices into every rank's next x",
+            "x1_max_rel_diff_vs_parity_y": diff, "pass": bool(diff <= 1e-12)}
+
+
 def main():
     args = parse()
+    run_watchdog = arm_run_watchdog(args)
     world, rank, local = setup_dist(args)
     dtype = np.float64 if args.dtype == "f64" else np.float32
     lib = spmv_hw.load(dtype)
@@ -746,6 +937,7 @@ def main():
     stream = torch.cuda.current_stream()
 
     t_setup = time.perf_counter()
+    stage("build")
     rp, col, val, x, ncols, desc = build_workload(lib, args, world, rank)
     plan = spmv_hw.Plan.from_device(lib, rp, col, val, ncols, device=local, stream=stream)
     st = plan.stats()
@@ -758,10 +950,12 @@ def main():
         del rp, col, val
         torch.cuda.empty_cache()
 
+    stage("warmup")
     for _ in range(args.warmup):
         plan.run(x, y, stream)
     torch.cuda.synchronize()
 
+    stage("timed")
     # 1) eager: one host launch per step, the main kernel timed with HIP events on its stream
     #    (roofline.achieved; rocprofv3 sees the same launches)
     barrier(world)
@@ -791,12 +985,30 @@ def main():
     plan.run_graph(x, y, args.steps, stream)
     torch.cuda.synchronize()
     barrier(world)
-    ms = spmv_dist.max_over_ranks((time.perf_counter() - tg0) * 1e3 / args.steps, dev)
+    product_ms = spmv_dist.max_over_ranks((time.perf_counter() - tg0) * 1e3 / args.steps, dev)
+    product_form = ("behind" if st["format"] & 256 else "dag" if st["format"] & 512 else "serial")
+    # 3) step semantics. spmv_plan_run_graph pipelines a split plan's steps
+    #    (the N >= 4 slices: step k's combine rides in step k + 1's sweep launch), which only
+    #    independent SpMVs of the same x allow. `value` is the serial chain -- every step complete
+    #    before the next starts, like the one-GPU headline, whose plan has no combine (its replay
+    #    IS the serial chain) -- so the driver's N-GPU / 1-GPU ratio compares like with like.
+    if product_form == "serial":
+        ms = product_ms
+    else:
+        ms = serial_chain_ms(plan, x, y, args.steps, world, dev)
     graph = {"iters": args.steps, "ms_per_step": round(ms, 5), "timed": "headline (value, ms_per_step)",
              "eager_ms_per_step": round(eager_ms, 5),
-             # how the replay orders the steps (plan stats format bits 8 / 9)
-             "form": ("behind: each step's combine in the next step's sweep launch" if st["format"] & 256 else
-                      "dag: the combines on a second stream" if st["format"] & 512 else "serial")}
+             "value_form": "serial: each SpMV (sweep, then the combine of a split plan) ends before the next begins",
+             # how spmv_plan_run_graph orders the steps (plan stats format bits 8 / 9)
+             "run_graph_form": product_form, "run_graph_ms_per_step": round(product_ms, 5)}
+    step_forms = {"value_form": "serial", "serial_ms_per_step": round(ms, 5),
+                  "behind_ms_per_step": round(product_ms, 5) if product_form == "behind" else None,
+                  "independent_pipelined_ms_per_step": round(product_ms, 5),
+                  "dependent_ms_per_step": None,
+                  "note": "serial = value (K SpMVs of one x, each complete before the next); behind = "
+                          "spmv_plan_run_graph on a split plan (step k's combine inside step k + 1's sweep: "
+                          "independent SpMVs only); dependent = x <- A x with the all-gather exchange in every "
+                          "step (compute + exchange)"}
 
     xtiles = det = binned = None
     if want_xtiles:  # reported beside the headline, never fatal to it
@@ -938,6 +1150,7 @@ def main():
         "parity": None,
         "exchange": None,
         "graph": graph,
+        "step_forms": step_forms,
         "strong_companion": None,
         "weak_companion": None,
         "lds_xtiles": xtiles,
@@ -948,10 +1161,6 @@ def main():
         "plan": {k: st[k] for k in ("nr_tiles", "tile_nnz", "device_bytes", "kernel", "format", "nr_nonempty_rows")},
         "setup_s": round(setup_s, 2),
     }
-    # the line above is complete; what follows adds reported-only fields. Each runs under a
-    # try (reported, never fatal), and a watchdog prints the line as it stands and ends the
-    # process if they take longer than --extras-timeout seconds (a hung collective on an
-    # 8-GPU node must not cost the measured value)
     emitted = threading.Event()
 
     def emit(note=None):
@@ -959,6 +1168,30 @@ def main():
             emitted.set()
             line = dict(out, extras_timeout=note) if note else out
             print(json.dumps(line), flush=True)
+        stage("emitted" if rank == 0 else "done")
+
+    # N > 1: parity is part of the measurement, not an extra (main.cpp:77-82 verifies every
+    # spmv_hw result). It runs under the run deadline and the collective timeout only; a parity
+    # that errors or fails prints the line with it and ends the run with status 3.
+    held = {}
+    if os.environ.get("SPMV_BENCH_INJECT") == "parity" and rank == world - 1:
+        y[0] += 1.0  # test hook (tests/test_gpu_bench.py): a wrong y must fail the run
+    if args.multi:
+        stage("parity")
+        try:
+            out["parity"] = distributed_parity(lib, args, world, rank, dev, y, st, held)
+        except Exception as e:
+            out["parity"] = {"error": f"{type(e).__name__}: {str(e)[:300]}", "pass": False}
+        if not out["parity"].get("pass"):
+            emit()
+            print(f"bench.py rank {rank}: parity did not pass: {out['parity']}", file=sys.stderr, flush=True)
+            os._exit(3)
+
+    # what follows adds reported-only fields. Each runs under a try (reported, never fatal), and
+    # a watchdog prints the line as it stands and ends the process if they take longer than
+    # --extras-timeout seconds (a hung collective on an 8-GPU node must not cost the measured,
+    # verified value)
+    stage("extras")
 
     def on_timeout():
         emit(f"extras still running after {args.extras_timeout} s; line printed without them")
@@ -1057,9 +1290,21 @@ def main():
                 res["native"] = {"error": str(e)[:300]}
         return res
 
-    if args.multi:  # correctness first: the parity of this very run, then the side measurements
-        guarded("parity", lambda: distributed_parity(lib, args, world, rank, dev, y, st))
+    if args.multi and args.scaling == "strong" and args.workload == "powerlaw":
+        # the dependent form x <- A x (square matrix): compute + all-gather in every step
+        def dependent():
+            res = dependent_iteration(plan, x, y, st, args.steps, world, rank, dev, held.get("y_full"))
+            step_forms["dependent_ms_per_step"] = res["ms_per_step"]
+            return res
+        guarded("dependent", dependent)
+        step_forms["dependent"] = out.pop("dependent")
+    held.clear()
+    if args.multi:
         guarded("exchange", exchange_fields)
+        nat = out["exchange"].get("native") if isinstance(out["exchange"], dict) else None
+        if isinstance(nat, dict) and "allgather_graph_ms_per_step" in nat:
+            # the same dependent form through the library's own RCCL clique, steps in one hipGraph
+            step_forms["dependent_native_graph_ms_per_step"] = nat["allgather_graph_ms_per_step"]
     if args.multi and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
         guarded("strong_companion", lambda: strong_companion(lib, args, world, rank, dev, stream))
     if args.multi and args.scaling == "strong" and args.workload == "powerlaw" and not args.no_weak_companion:
@@ -1075,9 +1320,15 @@ def main():
         guarded("side_configs", lambda: {name: side_config(args, name, dev, stream) for name in ("config2", "config5")})
     watchdog.cancel()
     emit()
+    par = out.get("parity")
+    if isinstance(par, dict) and par.get("pass") is False:  # N = 1: the full-size check failed
+        print(f"bench.py: parity did not pass: {par}", file=sys.stderr, flush=True)
+        os._exit(3)
     plan.destroy()
     if dist.is_initialized():
         dist.destroy_process_group()
+    if run_watchdog is not None:
+        run_watchdog.cancel()
 
 
 if __name__ == "__main__":

@@ -114,8 +114,9 @@ typedef struct spmv_plan_stats {
                                     behind the next sweep launch; bit 9: the same with the
                                     combines on a second stream (split plans, 2+ steps);
                                     bits 10 / 11: the pieces of a split sweep plan are cut with
-                                    the even / the odd XCCs' units lighter (the cut the build
-                                    timed fastest on this GPU, or env SPMV_SWEEP_XCC_BIAS) */
+                                    the even / the odd XCCs' units lighter (env
+                                    SPMV_SWEEP_XCC_BIAS > 0 / < 0; the default cuts them evenly,
+                                    so a plan's layout depends only on the matrix and the chip) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are
@@ -143,24 +144,15 @@ int spmv_plan_run(const spmv_plan *plan, const ValueType *d_x, ValueType *d_y, v
  * has run. */
 int spmv_plan_run_graph(spmv_plan *plan, const ValueType *d_x, ValueType *d_y, int iters, void *stream);
 int spmv_plan_get_stats(const spmv_plan *plan, spmv_plan_stats *stats);
-/* Kernel variants (performance experiments; every variant computes the same y).
- * Tile kernel: bit 0 = non-temporal streamed loads, bit 1 = non-temporal y stores (default 0).
- * Sweep kernel, packed entries: 15/20/22 = 2/4/8 entry groups per wave per workgroup barrier;
- * 26-34 = no barrier, waves run at most 1-4 iterations ahead of the slowest wave of the
- * workgroup (26: 4 groups lag 1, 27: 4/2, 28: 2/2 = default, 29: 2/4, 30: 2/1, 31: 3/2,
- * 32: 1/2, 33: 1/4, 34: 2/3; on a plan with delta-coded columns, stats format bit 6, the default
- * reads 11-byte entries and 35 runs it on the 12-byte words instead; 36 = the default; 37-39:
- * measurement-only work stealing among a split plan's pieces, tools library only); 50-63: measurement-only ablations of the tools library, refused
- * here (binned: 51-52). 94 (packed or unpacked): the deterministic kernel of
- * SPMV_SWEEP_DETERMINISTIC=1 (LDS adds in a fixed order, bitwise reproducible y; each wave's
- * adds complete before a release hand-over); 91: the same with a compiler-ordered hand-over
- * (3 % faster; relies on the LDS executing a CU's requests in arrival order). Unpacked entries (a chunk spans >= 65536 columns):
- * 0/1/3/7/15/22 and the default (4 groups of 2 per barrier). Slices (kernel 5): 0 = 4 slot
- * pairs per iteration (default), 1 = 2, 2 = 7, 3 = 4 re-reading past the slice's end.
- * Blocked (kernel 4): 1 = measurement-only ablation, partials stored in compact order (wrong y).
- * Binned (kernel 6): 1 / 2 = segment offsets rebased past 2^31 / 2^32 (tests; same y), 3 / 4 / 5 =
- * pass 1 with temporal product stores / entry loads / both, 6 = non-temporal product stores
- * (same y; 0 = the plan's choice: temporal stores when the products take <= 1 GiB). */
+/* Kernel variants. The product library accepts: 0 = the plan's default kernel form (every
+ * kernel; for the sweep the same as 28), sweep 94 = the deterministic kernel of
+ * SPMV_SWEEP_DETERMINISTIC=1 on any sweep plan (LDS adds in a fixed order, bitwise reproducible
+ * y), and binned (kernel 6) 1 / 2 = segment offsets rebased past 2^31 / 2^32 (the same y; the
+ * tests' handle on the 64-bit offset path). Any other variant returns an error ("tools library
+ * only"): the performance experiments (sweep 15-35 and 91, the unpacked sweep's forms, tile and
+ * slice load/store forms, binned cache policies 3-7) and the measurement-only ablations (some
+ * give a wrong y by design) are built only into the tools library (-DSPMV_ABLATIONS, Makefile
+ * target `ablations`). The reference exposes no tuning surface (csr_hw_wrapper.h:9-17). */
 int spmv_plan_set_variant(spmv_plan *plan, int variant);
 /* Per-plan kernel timing with HIP events recorded around the main kernel on the launch
  * stream: enable, then read back the mean duration (ms) and count of timed launches. */

@@ -115,7 +115,8 @@ struct spmv_mgpu {
     std::vector<ValueType *> y;         // rank 0 only: the full y
     std::vector<hipEvent_t> ev;         // per device: start, kernels done, exchange done
     double compute_ms = 0, exchange_ms = 0;
-    int rccl_calls = 0;                 // RCCL calls (schedule exchange ops) the last run issued
+    int rccl_calls = 0;                 // RCCL calls per step of the last run, all local devices
+                                        // (the schedule's exchange ops; run, _pipelined and _graph)
     // spmv_mgpu_run_pipelined: per device a second stream for the exchange, a second y buffer
     // (and reduce partial), and the events that hand each buffer between the two streams
     struct Pipe {
@@ -238,13 +239,15 @@ static int schedule_of(const spmv_mgpu *mg, int d, int exchange, std::vector<spm
     return 0;
 }
 
-static bool has_exchange(const std::vector<spmv_xop> &ops)
+static int exchange_ops(const std::vector<spmv_xop> &ops)
 {
+    int n = 0;
     for (const spmv_xop &o : ops)
-        if (o.kind >= SPMV_XOP_SEND)
-            return true;
-    return false;
+        n += o.kind >= SPMV_XOP_SEND;
+    return n;
 }
+
+static bool has_exchange(const std::vector<spmv_xop> &ops) { return exchange_ops(ops) > 0; }
 
 // the local ops (ZERO, COMPUTE) of device d on its compute stream s
 static int issue_local(spmv_mgpu *mg, int d, const std::vector<spmv_xop> &ops, const XBufs &b, const ValueType *x,
@@ -595,14 +598,13 @@ int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev)
         SPMV_TRY(hipEventRecord(mg->ev[3 * d + 1], s));
     }
     mg->rccl_calls = 0;
+    for (int d = 0; d < nl; ++d)
+        mg->rccl_calls += exchange_ops(sch[d]);
     if (any) {
         MG_NCCL(mg->nc->GroupStart());
-        for (int d = 0; d < nl; ++d) {
+        for (int d = 0; d < nl; ++d)
             if (issue_exchange(mg, d, sch[d], bufs(d), mg->stream[d]))
                 return 1;
-            for (const spmv_xop &o : sch[d])
-                mg->rccl_calls += o.kind >= SPMV_XOP_SEND;
-        }
         MG_NCCL(mg->nc->GroupEnd());
     }
     double cmax = 0, tmax = 0;
@@ -691,6 +693,9 @@ int spmv_mgpu_run_pipelined(spmv_mgpu *mg, int exchange, int steps, double *ms_p
             return 1;
         any = any || has_exchange(sch[d]);
     }
+    mg->rccl_calls = 0;
+    for (int d = 0; d < nl; ++d)
+        mg->rccl_calls += exchange_ops(sch[d]);
     for (int d = 0; d < nl; ++d) {
         SPMV_TRY(hipSetDevice(mg->dev[d]));
         SPMV_TRY(hipEventRecord(mg->pipe[d].t0, mg->stream[d]));
@@ -795,6 +800,12 @@ int spmv_mgpu_run_graph(spmv_mgpu *mg, int exchange, int iters, double *ms_per_s
     if (exchange == 2 && !mg->xnext[0])
         SPMV_TRY(hipMalloc((void **)&mg->xnext[0], nb));
     hipStream_t s = mg->stream[0];
+    {
+        std::vector<spmv_xop> ops;
+        if (schedule_of(mg, 0, exchange, ops))
+            return 1;
+        mg->rccl_calls = exchange_ops(ops);  // per step; the graph replays them every step
+    }
     if (!mg->gexec || mg->g_exchange != exchange || mg->g_iters != iters || mg->g_x != mg->x[0]) {
         if (mg->gexec) {
             SPMV_TRY(hipGraphExecDestroy(mg->gexec));

@@ -402,8 +402,6 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
     // failure here only means the first run loads them)
     if (P.kernel == kKernelSweep) {
         (void)launch_sweep(P, nullptr, nullptr, s, true);
-        if (sweep_tune_bias(P, s))
-            return 1;
     } else if (P.kernel == kKernelBinned) {
         (void)launch_binned(P, nullptr, nullptr, s, true);
     } else if (P.kernel == kKernelBlocked) {
@@ -636,6 +634,18 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     }
     *out = p.release();
     return 0;
+}
+
+// the variants the product library accepts, per kernel (spmv_plan_set_variant)
+bool product_variant(int kernel, int variant)
+{
+    if (variant == 0)
+        return true;
+    if (kernel == kKernelSweep)
+        return variant == 28 || variant == kSweepTurnOrdered;
+    if (kernel == kKernelBinned)
+        return variant == 1 || variant == 2;
+    return false;
 }
 
 }  // namespace spmvhw
@@ -1043,14 +1053,19 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
         return 1;
     }
 #ifndef SPMV_ABLATIONS
-    // the measurement-only ablations (some give a wrong y by design) exist only in the tools
-    // library built with -DSPMV_ABLATIONS (Makefile target `ablations`, tools/ab_variants.py)
-    if ((p->kernel == kKernelSweep && ((variant >= 50 && variant <= 63) || (variant >= 37 && variant <= 39))) ||
-        (p->kernel == kKernelBlocked && variant == 1) ||
-        (p->kernel == kKernelBinned && variant >= 51 && variant <= 52)) {
-        set_error("spmv_plan_set_variant: measurement-only ablation variant (tools library only)");
+    // The product library takes only what a caller needs (the reference exposes no tuning
+    // surface, csr_hw_wrapper.h:9-17): 0 = the plan's default kernel form (the sweep's default is
+    // 28, also accepted by number), the sweep's deterministic kernel 94 (bitwise reproducible y,
+    // the form of SPMV_SWEEP_DETERMINISTIC=1), and binned 1 / 2 (segment offsets rebased past
+    // 2^31 / 2^32: the same y, for the tests of the 64-bit offset path). Every other variant is a
+    // performance experiment or an ablation (some give a wrong y by design) and exists only in
+    // the tools library built with -DSPMV_ABLATIONS (Makefile target `ablations`).
+    if (!product_variant(p->kernel, variant)) {
+        set_error("spmv_plan_set_variant: measurement variant (tools library only)");
         return 1;
     }
+    if (p->kernel == kKernelSweep && variant == 0)
+        variant = 28;
 #endif
     if (p->kernel == kKernelSweep) {
         // every variant but the default (28), 36 (the same) and the measurement build's stealing

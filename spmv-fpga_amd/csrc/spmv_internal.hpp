@@ -140,9 +140,7 @@ struct spmv_plan {
                                        // that step k + 1's sweep can run while step k's partials wait
                                        // for their combine
     uint32_t *d_gcount = nullptr;      // spmv_plan_run_graph, "behind" form: two chunk counters
-    bool xbias_tune = false;           // split plan: sweep_tune_bias picks the pieces' XCC bias
-    double xbias_split = 0.0;          // the pieces' XCC bias in use (split plans)
-    std::vector<uint32_t> h_poff, h_punit;  // until the tuning: panel entry offsets, first units
+    double xbias_split = 0.0;          // the pieces' XCC bias in use (split plans; env SPMV_SWEEP_XCC_BIAS)
     unsigned long long *d_steal = nullptr;  // tools build, split > 1: per unit, iterations claimed
                                             // from the front (low word) and back (high word) by the
                                             // work-stealing variants 37-39; re-armed by k_sweep_combine
@@ -287,7 +285,7 @@ struct sweep_behind {
 hipError_t launch_sweep(const spmv_plan &p, const ValueType *d_x, ValueType *d_y, hipStream_t s, bool warm = false,
                         int phase = 0, void *part = nullptr, const sweep_behind *behind = nullptr);
 bool sweep_behind_ok(const spmv_plan &p);  // the plan's sweep launch can carry a combine behind
-int sweep_tune_bias(spmv_plan &p, hipStream_t s);  // split plans: time three XCC-bias cuts, keep the best
+bool product_variant(int kernel, int variant);  // spmv_plan_set_variant: accepted by the product library
 // 0 ok, 1 error, 2 the padded layout would overflow 32-bit entry offsets (caller may use tiles)
 int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src, const ValueType *d_val_src,
                 hipStream_t s);
@@ -308,7 +306,7 @@ int mgpu_create_borrowed(spmv_mgpu **out, int n, const int *devices, const Index
                          const spmv_plan *const *plans);
 int mgpu_run_on(spmv_mgpu *mg, int exchange, const ValueType *const *x_dev);
 const ValueType *mgpu_root_y(const spmv_mgpu *mg);
-int mgpu_rccl_calls(const spmv_mgpu *mg);  // RCCL calls the last mgpu_run_on issued
+int mgpu_rccl_calls(const spmv_mgpu *mg);  // RCCL calls per step of the last run (run, _pipelined, _graph)
 }  // namespace spmvhw
 
 #define SPMV_TRY(expr)                                                                        \

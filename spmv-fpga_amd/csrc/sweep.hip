@@ -1177,14 +1177,15 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     if (p.sweep_det || p.sweep_variant == kSweepTurn || p.sweep_variant == kSweepTurnOrdered) {
         // ORD 0 (each wave's adds complete before the release hand-over) is the default of
         // SPMV_SWEEP_DETERMINISTIC=1: its ordering follows from the memory model alone. Variant 91
-        // keeps the 3 % faster ORD 1 hand-over (compiler ordering; relies on the LDS executing a
-        // CU's requests in arrival order) for measurements.
-        const bool ord0 = p.sweep_variant != kSweepTurn;
-        if (p.sweep_packed) {
-            if (ord0) TURN(true, 0); else TURN(true, 1);
-        } else {
-            if (ord0) TURN(false, 0); else TURN(false, 1);
+        // (tools library) keeps the 3 % faster ORD 1 hand-over (compiler ordering; relies on the
+        // LDS executing a CU's requests in arrival order) for measurements.
+#ifdef SPMV_ABLATIONS
+        if (p.sweep_variant == kSweepTurn) {
+            if (p.sweep_packed) TURN(true, 1); else TURN(false, 1);
+            return;
         }
+#endif
+        if (p.sweep_packed) TURN(true, 0); else TURN(false, 0);
         return;
     }
 #undef TURN
@@ -1202,8 +1203,11 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
                        (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels, bh.rows_per_thread)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
-        // 15/20/22: 2/4/8 groups per barrier; 26-34: loose sync, Q groups, lag (default 28)
         switch (p.sweep_variant) {
+#ifdef SPMV_ABLATIONS
+        // measurement variants (tools library): 15/20/22: 2/4/8 groups per barrier; 26-34: loose
+        // sync, Q groups, lag (the default is 28: 2 groups, lag 2); 35: the default on the
+        // 12-byte rc words of a delta plan
         case 15: PK(2, 0); break;
         case 20: PK(4, 0); break;
         case 22: PK(8, 0); break;
@@ -1215,9 +1219,8 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 32: PK(1, 2); break;
         case 33: PK(1, 4); break;
         case 34: PK(2, 3); break;
-#ifdef SPMV_ABLATIONS
-        // measurement-only ablations, built only into the tools library (Makefile target
-        // `ablations`); 54, 55 and 60-63 give a wrong y by design, DESIGN.md §4
+        case 35: PK(2, 2); break;
+        // measurement-only ablations; 54, 55 and 60-63 give a wrong y by design, DESIGN.md §4
         case 60: if (p.nr_cols >= 32768) { PKA(1); } else { PK(2, 2); } break;  // x gathers all L2 hits
         case 61: PKA(2); break;  // no x gathers
         case 62: PKA(3); break;  // entries from L2 (first 4K of the unit), real gathers
@@ -1231,7 +1234,6 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         case 53: PKA(10); break;  // half the value bytes: 8 B/entry streamed instead of 12
         case 50: if (p.panel_rmax >= 16384) { PKA(11); } else { PK(2, 2); } break;  // 11-B entries + delta decode
 #endif
-        case 35: PK(2, 2); break;  // variant 28 on the 12-byte rc words of a delta plan (A/B)
         default:
             if (p.sweep_delta) {
 #ifdef SPMV_ABLATIONS
@@ -1257,12 +1259,14 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
         return;
     }
     switch (p.sweep_variant) {
-    case 0: SWEEP(4, 1, false, false); break;
+#ifdef SPMV_ABLATIONS
+    case 0: SWEEP(4, 1, false, false); break;  // measurement variants of the unpacked form
     case 1: SWEEP(4, 1, false, true); break;
     case 3: SWEEP(4, 1, true, true); break;
     case 7: SWEEP(4, 2, true, true); break;
     case 15: SWEEP(2, 2, true, true); break;
     case 22: SWEEP(2, 8, true, true); break;
+#endif
     default: SWEEP(2, 4, true, true); break;  // best unpacked form (0.88 ms on the 10M/160M matrix)
     }
 #undef SWEEP
@@ -1343,75 +1347,6 @@ static void cut_units(const std::vector<uint32_t> &poff, const std::vector<uint3
     uent[U] = poff[P];
 }
 
-// Split plans: which XCCs sweep slower is a property of the GPU, not of the matrix (even ones on
-// the boxes of round 3, odd ones on some of round 4: DESIGN.md §6), and the pieces' cut is cheap
-// to redo (unit_ent only). So the build times three cuts of the pieces -- even XCCs lighter by
-// 2 %, even, odd lighter by 2 % -- interleaved (3 rounds of 3 SpMVs each, on scratch x / y)
-// and keeps the fastest. A few ms per plan.
-int sweep_tune_bias(spmv_plan &p, hipStream_t s)
-{
-    if (!p.xbias_tune || p.sweep_det)
-        return 0;
-    const double cand[3] = {0.02, 0.0, -0.02};
-    ValueType *x = nullptr, *y = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    std::vector<uint32_t> uent;
-    float best = -1.0f, t[3][3] = {};
-    int pick = 0;
-    hipError_t err = hipMalloc((void **)&x, std::max<uint64_t>(p.nr_cols, 1) * sizeof(ValueType));
-    if (err == hipSuccess)
-        err = hipMalloc((void **)&y, std::max<uint64_t>(p.nr_rows, 1) * sizeof(ValueType));
-    if (err == hipSuccess)
-        err = hipMemsetAsync(x, 0, std::max<uint64_t>(p.nr_cols, 1) * sizeof(ValueType), s);
-    if (err == hipSuccess)
-        err = hipEventCreate(&e0);
-    if (err == hipSuccess)
-        err = hipEventCreate(&e1);
-    for (int r = 0; r < 3 && err == hipSuccess; ++r)
-        for (int c = 0; c < 3 && err == hipSuccess; ++c) {
-            cut_units(p.h_poff, p.h_punit, cand[c], uent);
-            err = hipMemcpy(p.d_unit_ent, uent.data(), uent.size() * 4, hipMemcpyHostToDevice);
-            if (err == hipSuccess)
-                err = launch_sweep(p, x, y, s);  // warm this cut
-            if (err == hipSuccess)
-                err = hipEventRecord(e0, s);
-            for (int k = 0; k < 3 && err == hipSuccess; ++k)
-                err = launch_sweep(p, x, y, s);
-            if (err == hipSuccess)
-                err = hipEventRecord(e1, s);
-            if (err == hipSuccess)
-                err = hipEventSynchronize(e1);
-            if (err == hipSuccess)
-                err = hipEventElapsedTime(&t[c][r], e0, e1);
-        }
-    if (err == hipSuccess) {
-        for (int c = 0; c < 3; ++c) {
-            float m[3] = {t[c][0], t[c][1], t[c][2]};
-            std::sort(m, m + 3);
-            if (best < 0.0f || m[1] < best)
-                best = m[1], pick = c;
-        }
-        cut_units(p.h_poff, p.h_punit, cand[pick], uent);
-        err = hipMemcpy(p.d_unit_ent, uent.data(), uent.size() * 4, hipMemcpyHostToDevice);
-        p.xbias_split = cand[pick];
-    }
-    if (e0)
-        (void)hipEventDestroy(e0);
-    if (e1)
-        (void)hipEventDestroy(e1);
-    if (x)
-        (void)hipFree(x);
-    if (y)
-        (void)hipFree(y);
-    p.h_poff.clear();
-    p.h_punit.clear();
-    if (err != hipSuccess) {
-        set_error(std::string("build_sweep: bias tuning: ") + hipGetErrorString(err));
-        return 1;
-    }
-    return 0;
-}
-
 // Host: panel boundaries (nnz-balanced, <= rmax rows each), then the device sort + scatter.
 // Work units: when the slice has at least one panel per resident workgroup, panels are rounded
 // to whole rounds of workgroups and each panel is one unit. When it has fewer (a slice of fewer
@@ -1458,8 +1393,13 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     // Defaults on a whole chip (256 CUs = 8 XCDs): d = 0.015 for whole panels, 0.02 for split
     // pieces (interleaved A/B, profiles/r03bb_xcc_bias.jsonl: 10M/160M -1.3 %, the N = 8 slice
     // -2.0 %, N = 4 -0.7 %); env SPMV_SWEEP_XCC_BIAS=d overrides both (0 = even cut).
+    // Split pieces (the N >= 4 strong-scaling slices) are cut evenly by default: which XCCs
+    // sweep slower varies from box to box (even ones on the boxes of round 3, odd ones on some of
+    // round 4), and the even cut was within 1 % of a per-GPU timed pick and ahead of the fixed
+    // 2 % bias at N = 4 (profiles/r04w_xcc_bias_ab.jsonl, r04y), a tie at N = 8. The cut is a
+    // function of the matrix and the chip's CU count only, like the reference's (csr_hw.cpp:459-468).
     const char *xbenv = std::getenv("SPMV_SWEEP_XCC_BIAS");
-    double xbias_split = xbenv ? std::atof(xbenv) : chip_cus == 256 ? 0.02 : 0.0;
+    double xbias_split = xbenv ? std::atof(xbenv) : 0.0;
     double xbias = xbenv ? std::atof(xbenv) : chip_cus == 256 ? 0.015 : 0.0;
     if (!(xbias > -0.5 && xbias < 0.5))
         xbias = xbias_split = 0.0;
@@ -1558,12 +1498,6 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     }
     cut_units(poff, punit, split_mode ? xbias : 0.0, uent);
     p.xbias_split = split_mode ? xbias : 0.0;
-    // a split plan on a whole chip whose bias no env pins: sweep_tune_bias picks it on this GPU
-    p.xbias_tune = split_mode && multi && !xbenv && chip_cus == 256 && !det;
-    if (p.xbias_tune) {
-        p.h_poff = poff;
-        p.h_punit = punit;
-    }
     p.sweep_split = multi ? std::max<uint32_t>(split, 2) : 1;  // > 1: combine kernel needed
     p.nunits = U;
     if (multi) {

@@ -280,7 +280,63 @@ def test_deterministic_kernel_ships_only_its_ordered_forms(dtype):
     turns = [ln for ln in out.splitlines() if "k_spmv_sweep_turn<" in ln]
     assert turns
     ords = {ln.split("k_spmv_sweep_turn<", 1)[1].split(">", 1)[0].split(", ")[4] for ln in turns}
-    assert ords == {"0", "1"}, ords
+    assert ords == {"0"}, ords  # ORD 1 (variant 91) is a measurement variant: tools library
+
+
+# what spmv_plan_set_variant accepts in the product library, per kernel (plan.cpp product_variant)
+PRODUCT_VARIANTS = {"tiles": {0}, "gold": {0}, "sweep": {0, 28, 94}, "fpga": {0}, "blocked": {0},
+                    "slices": {0}, "binned": {0, 1, 2}}
+KERNEL_IDS = {"tiles": 0, "gold": 1, "sweep": 2, "fpga": 3, "blocked": 4, "slices": 5, "binned": 6}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", sorted(PRODUCT_VARIANTS))
+def test_product_refuses_every_measurement_variant(monkeypatch, kernel):
+    """the product library's variant surface is the default, the deterministic
+    sweep (94) and the binned kernel's test rebases (1 / 2); every other variant in 0..127 is
+    refused with "tools library only" (or "bad arguments" past 63), on a plan of every kernel.
+    The plan still runs afterwards and matches the oracle."""
+    import torch
+    import oracle
+    monkeypatch.setenv("SPMV_HW_KERNEL", kernel)
+    lib = spmv_hw.load(np.float64, ablations=False)
+    n, z = 20_000, 320_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+    assert plan.stats()["kernel"] == KERNEL_IDS[kernel]
+    accepted = set()
+    for v in range(128):
+        try:
+            plan.set_variant(v)
+            accepted.add(v)
+        except RuntimeError as e:
+            assert "tools library only" in str(e) or (v > 63 and "bad arguments" in str(e)), (v, str(e))
+    assert accepted == PRODUCT_VARIANTS[kernel], sorted(accepted)
+    plan.set_variant(0)
+    y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
+    plan.run(x, y)
+    torch.cuda.synchronize()
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    r, c = h[0].view(np.uint32), h[1].view(np.uint32)
+    ref = oracle.spmv_gold(r, c, h[2], h[3])
+    assert oracle.scaled_error(r, c, h[2], h[3], ref, y.cpu().numpy()) <= 1e-12
+    plan.destroy()
+
+
+def test_product_variant_table_matches_the_source():
+    """The CPU side of the same check: plan.cpp's product_variant lists exactly the variants above
+    (the measurement variants' kernel forms are compiled only under -DSPMV_ABLATIONS)."""
+    src = open(os.path.join(ROOT, "spmv-fpga_amd", "csrc", "plan.cpp")).read()
+    body = src[src.index("bool product_variant(int kernel, int variant)"):]
+    body = body[:body.index("\n}\n")]
+    assert "variant == 0" in body
+    assert "kKernelSweep)\n        return variant == 28 || variant == kSweepTurnOrdered;" in body
+    assert "kKernelBinned)\n        return variant == 1 || variant == 2;" in body
+    assert body.rstrip().endswith("return false;")
+    sweep = open(os.path.join(ROOT, "spmv-fpga_amd", "csrc", "sweep.hip")).read()
+    head = sweep[:sweep.index("case 15: PK(2, 0); break;")]
+    assert head.rfind("#ifdef SPMV_ABLATIONS") > head.rfind("#endif")
 
 
 DOCUMENTED_ENV = {"SPMV_NGPUS", "SPMV_HW_MERGE", "SPMV_HW_KERNEL", "SPMV_FPGA_VF", "SPMV_FPGA_BLOCK",

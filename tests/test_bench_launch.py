@@ -53,6 +53,48 @@ def test_self_launch_stops_a_hung_rank_after_another_failed():
     assert p.returncode == 137, (p.returncode, p.stderr)
 
 
+def test_self_launch_all_ranks_hung_end_at_the_run_timeout():
+    """every rank stuck (e.g. in one collective) -- no rank ever exits. The
+    parent's --run-timeout kills them all, prints one JSON error line naming each rank's last
+    stage, and exits 124, well before the driver's own limit."""
+    p = _run("--gpus", "3", "--dry-launch", "--dry-launch-rc", "0:hang,1:hang,2:hang", "--run-timeout", "3",
+             timeout=60)
+    assert p.returncode == 124, (p.returncode, p.stderr)
+    (line,) = [ln for ln in _lines(p.stdout) if "error" in ln]  # (rank 0's dry-launch line aside)
+    assert line["value"] is None and "run timeout" in line["error"] and line["rc"] == 124
+    assert line["stage"] == {"0": "timed", "1": "timed", "2": "timed"}, line
+
+
+def test_self_launch_rank0_done_others_hung():
+    """rank 0 finished (its line printed, status 0) but a peer never exits: after
+    --spawn-grace the parent kills it and fails; rank 0's line stays the only stdout line."""
+    p = _run("--gpus", "3", "--dry-launch", "--dry-launch-rc", "2:hang", "--spawn-grace", "1", timeout=60)
+    assert p.returncode == 137, (p.returncode, p.stderr)
+    (line,) = _lines(p.stdout)
+    assert line["RANK"] == "0" and "dry_launch" in line
+    assert "killed as hung" in p.stderr
+
+
+def test_self_launch_failed_rank0_gets_an_error_line():
+    """Rank 0 failed before printing its line: the parent prints the error line (stages, statuses)."""
+    p = _run("--gpus", "2", "--dry-launch", "--dry-launch-rc", "0:5", timeout=60)
+    assert p.returncode == 5, (p.returncode, p.stderr)
+    lines = _lines(p.stdout)
+    err = [ln for ln in lines if "error" in ln]
+    assert len(err) == 1 and err[0]["value"] is None and err[0]["stage"]["0"] == "init", lines
+
+
+def test_under_a_launcher_the_rank_has_its_own_deadline():
+    """torch.distributed.run starts the ranks (no bench.py parent): each rank's own --run-timeout
+    ends a hang with status 124, rank 0 printing the error line."""
+    p = _run("--gpus", "2", "--dry-launch", "--dry-launch-rc", "0:hang", "--run-timeout", "2",
+             env={"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": "29999"}, timeout=60)
+    assert p.returncode == 124, (p.returncode, p.stderr)
+    lines = _lines(p.stdout)
+    assert lines[-1]["value"] is None and lines[-1]["stage"] == {"0": "timed"}, lines
+
+
 def test_under_a_launcher_no_second_spawn():
     """With WORLD_SIZE set (torch.distributed.run), bench.py is one rank and starts nothing."""
     p = _run("--gpus", "2", "--dry-launch",

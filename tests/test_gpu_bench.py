@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 SMALL = ["--rows", "400000", "--nnz", "6400000", "--steps", "3", "--warmup", "1", "--extras-timeout", "150"]
 
 
-def _bench(*args, env=None):
+def _bench(*args, env=None, want_rc=0):
     e = {k: v for k, v in os.environ.items()
          if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     e.update(env or {})
@@ -33,7 +33,7 @@ def _bench(*args, env=None):
         os.killpg(p.pid, signal.SIGKILL)
         out, err = p.communicate()
         pytest.fail("bench.py timed out: " + err[-4000:])
-    assert p.returncode == 0, out[-2000:] + err[-4000:]
+    assert p.returncode == want_rc, out[-2000:] + err[-4000:]
     lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out[-2000:]
     return lines[0]
@@ -49,6 +49,9 @@ def test_bench_one_gpu_line():
     assert r["kernel_ms_per_rank"] == [r["kernel_ms"]]
     assert d["cpu_baseline"]["cores"] == 1 and d["cpu_baseline"]["kind"] == "port"
     assert d["parity"]["pass"] and d["parity"]["max_scaled_err"] <= 1e-12
+    sf = d["step_forms"]  # value is the serial chain (each SpMV complete before the next)
+    assert sf["value_form"] == "serial" and sf["serial_ms_per_step"] == d["ms_per_step"]
+    assert d["graph"]["run_graph_ms_per_step"] > 0
 
 
 @pytest.mark.parametrize("scaling", ["strong", "weak"])
@@ -63,6 +66,17 @@ def test_bench_two_ranks_self_launched(scaling):
     if scaling == "strong":
         assert d["config"]["slice_rows"][0] == 0
         assert d["exchange"]["backend"] == "gloo" and d["exchange"]["pipelined_max_rel_diff"] == 0.0
+        sf = d["step_forms"]
+        assert sf["value_form"] == "serial" and sf["serial_ms_per_step"] == d["ms_per_step"]
+        assert sf["dependent"]["pass"] and sf["dependent_ms_per_step"] > 0, sf
+
+
+def test_bench_parity_failure_fails_the_run():
+    """at N > 1 parity is not an extra. A wrong y on the last rank (test hook
+    SPMV_BENCH_INJECT=parity) prints the line with the failed parity and exits 3."""
+    d = _bench("--gpus", "2", "--no-weak-companion", "--no-native-exchange",
+               env={"SPMV_BENCH_BACKEND": "gloo", "SPMV_BENCH_INJECT": "parity"}, want_rc=3)
+    assert d["n_ranks"] == 2 and d["parity"]["pass"] is False and d["parity"]["max_scaled_err"] > 1e-6
 
 
 @pytest.mark.parametrize("scaling", ["strong", "weak"])
@@ -80,3 +94,6 @@ def test_bench_one_rank_rccl_rehearsal(scaling):
         assert "error" not in nat, nat
         assert nat["rccl_comm_count"] == 1 and nat["gather_max_rel_diff_vs_torch"] <= 1e-12  # two SpMVs (LDS adds)
         assert all(nat[k] > 0 for k in ("gather_compute_ms", "reduce_exchange_ms", "allgather_graph_ms_per_step"))
+        sf = d["step_forms"]
+        assert sf["dependent"]["pass"] and sf["dependent_ms_per_step"] > 0
+        assert sf["dependent_native_graph_ms_per_step"] == nat["allgather_graph_ms_per_step"]

@@ -1098,7 +1098,7 @@ def test_sweep_delta_columns(torch, monkeypatch, dtype, shape):
     bucketed keys (shift 1), which the delta build re-sorts per chunk."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     monkeypatch.delenv("SPMV_SWEEP_DELTA", raising=False)
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=True)  # variant 35 below: tools library
     if shape == "powerlaw":
         n, m, z = 2_000_000, 10_000_000, 32_000_000
     else:
@@ -1134,7 +1134,7 @@ def test_sweep_delta_gap_edges(torch, monkeypatch, dtype):
     chunk (pad entries). y matches the oracle on the 11-byte and the 12-byte entries alike."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     monkeypatch.delenv("SPMV_SWEEP_DELTA", raising=False)
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=True)  # variant 35 below: tools library
     cyc = [0, 1, 255, 256, 511]
     gaps = [cyc[k % 5] for k in range(128)] + [cyc[k % 5] for k in range(127)] + [512] \
         + [(256, 511)[k % 2] for k in range(100)]
@@ -1244,16 +1244,20 @@ def test_measurement_layout_switches(torch, monkeypatch, dtype, knob):
     assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(dtype)]
 
 
-@pytest.mark.parametrize("bias", ["0", "0.1", "default"])
+@pytest.mark.parametrize("bias", ["0", "0.1", "0.02", "-0.02", "default"])
 @pytest.mark.parametrize("shape", ["panels", "pieces", "full"])
 def test_sweep_xcc_bias(torch, monkeypatch, shape, bias):
     """The sweep's XCC bias: units that run on even XCCs cut lighter than odd ones.
     'panels': 2M x 2M / 32M, whole panels (the biased panel cut); 'pieces': an N = 8-like slice,
-    1.25M x 10M / 20M, split pieces (the biased piece cut); 'full': the 10M/160M matrix, whose
-    panels sit within 5 % of the LDS row cap, so a 10 % bias clamps panels at the cap and then
-    falls back to the even cut. The unit count never changes, and y matches the oracle."""
+    1.25M x 10M / 20M, split pieces (the biased piece cut; the default cuts them evenly, and
+    stats format bit 10 / 11 names a pinned even- / odd-lighter cut); 'full': the 10M/160M
+    matrix, whose panels sit within 5 % of the LDS row cap, so a 10 % bias clamps panels at the
+    cap and then falls back to the even cut. The unit count never changes, and y matches the
+    oracle."""
     if shape == "full" and bias != "0.1":
         pytest.skip("the full matrix with the default cut runs in test_gpu_fullsize.py")
+    if shape == "panels" and bias in ("0.02", "-0.02"):
+        pytest.skip("whole panels: 0 and 0.1 cover the panel cut")
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
     if bias == "default":
         monkeypatch.delenv("SPMV_SWEEP_XCC_BIAS", raising=False)
@@ -1268,6 +1272,9 @@ def test_sweep_xcc_bias(torch, monkeypatch, shape, bias):
     st = plan.stats()
     assert st["kernel"] == 2, st
     assert st["nr_tiles"] == {"panels": 256, "pieces": 252, "full": 512}[shape], st
+    if shape == "pieces":
+        d = 0.0 if bias == "default" else float(bias)
+        assert bool(st["format"] & 1024) == (d > 0) and bool(st["format"] & 2048) == (d < 0), st
     y = torch.full((n,), float("nan"), dtype=x.dtype, device="cuda")
     plan.run(x, y)
     torch.cuda.synchronize()
@@ -1279,6 +1286,40 @@ def test_sweep_xcc_bias(torch, monkeypatch, shape, bias):
     assert not np.isnan(yy).any()
     ref = oracle.spmv_gold(row_ptr, c, v, xx)
     assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(np.float64)]
+
+
+@pytest.mark.parametrize("rank", [1, 3])
+def test_split_plan_build_is_reproducible(torch, monkeypatch, rank):
+    """a split sweep plan's layout is a function of the matrix and the chip
+    (the reference's cut is, csr_hw.cpp:459-468): the N = 4 slices of the 10M/160M matrix built
+    twice on one device give identical plan stats (format bits 10 / 11 included: the even default
+    cut), and both plans' y match the oracle."""
+    monkeypatch.delenv("SPMV_SWEEP_XCC_BIAS", raising=False)
+    monkeypatch.delenv("SPMV_HW_KERNEL", raising=False)
+    lib = spmv_hw.load(np.float64)
+    n = 10_000_000
+    rp_full, _ = lib.powerlaw_row_ptr(n, 160_000_000, 65536, 4)
+    b = lib.partition_rows(rp_full, 4)
+    r0, r1 = int(b[rank]), int(b[rank + 1])
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, 160_000_000, seed=4, row_begin=r0, row_end=r1)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    stats, ys = [], []
+    for _ in range(2):
+        plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
+        stats.append(plan.stats())
+        y = torch.full((r1 - r0,), float("nan"), dtype=x.dtype, device="cuda")
+        plan.run(x, y)
+        torch.cuda.synchronize()
+        ys.append(y.cpu().numpy())
+        plan.destroy()
+    assert stats[0] == stats[1], stats
+    st = stats[0]
+    assert st["kernel"] == 2 and not st["format"] & (1024 | 2048), st
+    h = [t.cpu().numpy() for t in (rp, col, val, x)]
+    row_ptr, c, v, xx = h[0].view(np.uint32), h[1].view(np.uint32), h[2], h[3]
+    ref = oracle.spmv_gold(row_ptr, c, v, xx)
+    for yy in ys:
+        assert oracle.scaled_error(row_ptr, c, v, xx, ref, yy) <= TIGHT[np.dtype(np.float64)]
 
 
 @pytest.mark.parametrize("bias", ["0.025", "0.2", "-0.1", "0"])

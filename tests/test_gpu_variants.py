@@ -1,8 +1,10 @@
-"""Kernel variants through the product library's C-ABI (spmv_plan_set_variant).
+"""Kernel variants through the C-ABI (spmv_plan_set_variant).
 
-VERDICT r1 item 6: the measurement-only ablations (sweep variants 51-63, blocked variant 1;
-several give a wrong y by design) exist only in the tools library built with -DSPMV_ABLATIONS
-(`make -C spmv-fpga_amd ablations`); the shipped library refuses them with an error code."""
+VERDICT r1 item 6 / r4 item 5: the product library accepts only the plan's default (0, and the
+sweep's 28), the deterministic sweep (94) and the binned test rebases (1 / 2); every performance
+experiment and measurement-only ablation (several give a wrong y by design) exists only in the
+tools library built with -DSPMV_ABLATIONS (`make -C spmv-fpga_amd ablations`), which these tests
+load for them. tests/test_abi.py checks the product's refusals kernel by kernel."""
 import numpy as np
 import pytest
 
@@ -12,9 +14,9 @@ from conftest import tools_env
 pytestmark = pytest.mark.gpu
 
 
-def _plan(monkeypatch, kernel, dtype=np.float64, n=50_000, z=800_000):
+def _plan(monkeypatch, kernel, dtype=np.float64, n=50_000, z=800_000, ablations=False):
     monkeypatch.setenv("SPMV_HW_KERNEL", kernel)
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=ablations)
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
     x = spmv_hw.gen_vector(lib, n, seed=6)
     return lib, spmv_hw.Plan.from_device(lib, rp, col, val, n), x
@@ -27,8 +29,8 @@ def test_sweep_ablation_variants_are_refused(monkeypatch, dtype):
     assert plan.stats()["kernel"] == 2
     y_ref = torch.empty(x.numel(), dtype=x.dtype, device="cuda")
     plan.run(x, y_ref)
-    for v in range(51, 64):
-        with pytest.raises(RuntimeError, match="measurement-only"):
+    for v in list(range(51, 64)) + [15, 34, 35, 91]:
+        with pytest.raises(RuntimeError, match="tools library only"):
             plan.set_variant(v)
     # the refusal leaves the plan on its previous (default) variant: same y, bit for bit up to
     # the LDS-atomic order (the sweep default is not bitwise reproducible)
@@ -37,15 +39,19 @@ def test_sweep_ablation_variants_are_refused(monkeypatch, dtype):
     torch.cuda.synchronize()
     rel = float(((y.double() - y_ref.double()).abs().max() / y_ref.double().abs().max()).item())
     assert rel < (1e-13 if dtype == np.float64 else 1e-6)
-    for v in (15, 28, 34):  # real variants are still accepted
+    for v in (0, 28, 94, 28):  # the default and the deterministic kernel are accepted
         plan.set_variant(v)
     plan.destroy()
+    _, tplan, _ = _plan(monkeypatch, "sweep", dtype, ablations=True)
+    for v in (15, 28, 34, 91):  # the measurement variants: tools library
+        tplan.set_variant(v)
+    tplan.destroy()
 
 
 def test_blocked_ablation_variant_is_refused(monkeypatch):
     lib, plan, x = _plan(monkeypatch, "blocked")
     assert plan.stats()["kernel"] == 4
-    with pytest.raises(RuntimeError, match="measurement-only"):
+    with pytest.raises(RuntimeError, match="tools library only"):
         plan.set_variant(1)
     plan.set_variant(0)
     plan.destroy()
@@ -140,7 +146,7 @@ def test_turn_sweep_is_bitwise_reproducible(monkeypatch, variant, n, z, dtype):
     import torch
     import oracle
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=variant == 91)  # 91: a measurement variant (tools library)
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
     x = spmv_hw.gen_vector(lib, n, seed=6)
     plan = spmv_hw.Plan.from_device(lib, rp, col, val, n)
@@ -191,7 +197,7 @@ def test_binned_segment_offsets_past_2_31(monkeypatch, dtype, variant, delta):
     torch.cuda.synchronize()
     err = oracle.scaled_error(r, c, h[2], h[3], ref, y.cpu().numpy())
     assert err <= (1e-12 if dtype == np.float64 else 2e-6), err
-    with pytest.raises(RuntimeError, match="binned variants"):
+    with pytest.raises(RuntimeError, match="tools library only"):
         plan.set_variant(8)
     plan.set_variant(0)
     plan.destroy()
@@ -201,12 +207,12 @@ def test_binned_segment_offsets_past_2_31(monkeypatch, dtype, variant, delta):
                                                           "mirrored"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_binned_pass1_cache_policy_variants(monkeypatch, dtype, variant):
-    """Binned variants 3-6 change only pass 1's cache policy (temporal product stores / entry
-    loads / both; 6: non-temporal stores), 7 where the products go (mirrored: stored down the
-    array, read back there by pass 2): y matches the oracle as with the default."""
+    """Binned variants 3-6 (tools library) change only pass 1's cache policy (temporal product
+    stores / entry loads / both; 6: non-temporal stores), 7 where the products go (mirrored:
+    stored down the array, read back there by pass 2): y matches the oracle as with the default."""
     import torch
     import oracle
-    lib, plan, x = _plan(monkeypatch, "binned", dtype, n=200_000, z=3_200_000)
+    lib, plan, x = _plan(monkeypatch, "binned", dtype, n=200_000, z=3_200_000, ablations=True)
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, 200_000, 200_000, 3_200_000, seed=4)
     h = [t.cpu().numpy() for t in (rp, col, val, x)]
     r, c = h[0].view(np.uint32), h[1].view(np.uint32)

@@ -51,18 +51,10 @@ def main():
     ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--cols", type=int, default=None, help="power-law: columns (default = rows)")
     a = ap.parse_args()
-    # measurement-only ablations live in the tools library only (spmv-fpga_amd Makefile target
-    # `ablations`); the product library refuses them
-    abl = any((v.split(":")[0].startswith("sweep") and int(v.split(":")[1]) in range(50, 64))
-              or (v.split(":")[0].startswith("blocked") and v.split(":")[1] == "1")
-              or (v.split(":")[0].startswith("binned") and int(v.split(":")[1]) in (51, 52))
-              for v in a.variants.split(",") if ":" in v)
-    # layout switches of a kernel spec (suffixes below) are read by the tools library only too
-    kerns = {v.split(":")[0].partition("#")[0] for v in a.variants.split(",") if ":" in v}
-    abl = abl or any("@" in k or "^" in k or (k.startswith("binned") and "~" in k)
-                     or k.rstrip("0123456789").endswith(("U", "S", "F", "X", "H", "W", "L", "F32")) for k in kerns)
-    if abl:
-        os.environ["SPMV_HW_ABLATIONS"] = "1"
+    # every variant but the default lives in the tools library (spmv-fpga_amd Makefile target
+    # `ablations`: the same kernels plus the measurement variants and layout switches); the
+    # product library refuses them
+    os.environ["SPMV_HW_ABLATIONS"] = "1"
     dtype = np.float64 if a.dtype == "f64" else np.float32
     lib = spmv_hw.load(dtype)
     variants = [v if ":" in v else f"tiles:{v}" for v in a.variants.split(",")]

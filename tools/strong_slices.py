@@ -41,7 +41,7 @@ def main():
                          "SPMV_GRAPH_FORM=serial|dag|behind, with _rN (SPMV_BEHIND_ROWS) / _bN (SPMV_BEHIND_BLOCKS)")
     a = ap.parse_args()
     dtype = np.float64 if a.dtype == "f64" else np.float32
-    lib = spmv_hw.load(dtype, ablations=bool(a.graph_ab) or None)
+    lib = spmv_hw.load(dtype, ablations=bool(a.graph_ab or a.variants) or None)
     n, z = a.rows, a.nnz
     rp_full, _ = lib.powerlaw_row_ptr(n, z, 65536, 4)
     x = spmv_hw.gen_vector(lib, n, seed=6)
