@@ -29,6 +29,7 @@ for s in $STEPS; do
     tests_sel) run pytest_sel 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     selflaunch) SPMV_BENCH_BACKEND=gloo run selflaunch_strong 600 python bench.py --gpus 2 --steps 5 --warmup 2 ;;
     selflaunch4) SPMV_BENCH_BACKEND=gloo run selflaunch4_strong 900 python bench.py --gpus 4 --steps 5 --warmup 2 --no-weak-companion ;;
+    selflaunch8) SPMV_BENCH_BACKEND=gloo run selflaunch8_strong 1000 python bench.py --gpus 8 ${SCALE_ARGS:-} ;;
     selflaunch_weak) SPMV_BENCH_BACKEND=gloo run selflaunch_weak 600 python bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak ;;
     abmirror) run abmirror 900 python tools/ab_variants.py --workload powerlaw --dtype f32 --rounds ${AB_ROUNDS:-7} --reps 10 \
                 --variants binned#1:0,binned#1:7,binned#2:0,binned#2:7,binned#3:0,binned#3:7,binned#4:0,binned#4:7 ;;
@@ -52,7 +53,6 @@ for s in $STEPS; do
     abbias) for i in $(seq 1 ${AB_ITERS:-3}); do
               SPMV_SWEEP_XCC_BIAS=0 run abbias0_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_0
               SPMV_SWEEP_XCC_BIAS=0.02 run abbiasd_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_0.02
-              run abbiast_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_tuned
             done ;;
     rccl1) run rccl1_strong 600 python bench.py --dist-rehearsal --scaling strong --no-weak-companion ;;
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak
