@@ -97,6 +97,9 @@ def parse(argv=None):
                     help="1 GPU: run the N > 1 code path as the one rank of an RCCL ('nccl') process "
                          "group -- its collectives, parity gather, exchange fields and the library's "
                          "own clique on the hardware (the path of the 8-GPU run, at world size 1)")
+    ap.add_argument("--slice-of", type=int, default=None,
+                    help="with --dist-rehearsal: the one rank holds rank 0's slice of an N-way strong cut "
+                         "(e.g. 8: the split plan, serial chain and behind form of an 8-GPU rank, over RCCL)")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the row-parallel CPU line (the box's CPU share is 16)")
@@ -118,6 +121,8 @@ def parse(argv=None):
     a = ap.parse_args(argv)
     if a.dist_rehearsal and a.gpus != 1:
         ap.error("--dist-rehearsal is the one-GPU form of the N > 1 path")
+    if a.slice_of is not None and not (a.dist_rehearsal and a.slice_of >= 1):
+        ap.error("--slice-of N needs --dist-rehearsal (and N >= 1)")
     if a.scaling is None:
         a.scaling = "strong" if a.gpus > 1 else "weak"
     a.multi = a.gpus > 1 or a.dist_rehearsal  # the N > 1 path: a process group, slices, exchange
@@ -362,7 +367,7 @@ def build_workload(lib, args, world, rank):
     z = args.nnz or 160_000_000
     if args.multi and args.scaling == "strong":
         rp_full, _ = lib.powerlaw_row_ptr(n, z, 65536, 4)
-        b = lib.partition_rows(rp_full, world)
+        b = lib.partition_rows(rp_full, args.slice_of or world)
         r0, r1 = spmv_dist.row_slice(b, rank)
         rp, col, val, scale = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4, row_begin=r0, row_end=r1)
         desc = {"workload": "powerlaw", "rows": n, "cols": n, "nnz": z, "slice_rows": [r0, r1]}
@@ -692,8 +697,9 @@ def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
     res = {"api": "spmv_mgpu_create_rank + spmv_mgpu_run (library RCCL clique, one rank per GPU)",
            "rccl_comm_count": mg.comm_count()}
     mg.set_x_device(x)
-    for name, mode in (("gather", spmv_hw.MGPU_GATHER), ("reduce", spmv_hw.MGPU_REDUCE),
-                       ("allgather", spmv_hw.MGPU_ALLGATHER)):
+    square = int(counts.sum()) == int(ncols)  # (--slice-of: the slices do not cover x; no all-gather)
+    forms = [("gather", spmv_hw.MGPU_GATHER), ("reduce", spmv_hw.MGPU_REDUCE)]
+    for name, mode in forms + ([("allgather", spmv_hw.MGPU_ALLGATHER)] if square else []):
         if mode == spmv_hw.MGPU_ALLGATHER:
             mg.set_x_device(x)
         for _ in range(2):
@@ -723,11 +729,12 @@ def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
                     ((y_n.double() - y_t.double()).abs().max() / y_t.double().abs().max().clamp_min(1e-300)).item())
     # iterative use: SpMV + all-gather of y into every rank's next x, steps
     # replayed from one hipGraph per rank (spmv_mgpu_run_graph; capture outside the timing)
-    mg.set_x_device(x)
-    mg.run_graph(spmv_hw.MGPU_ALLGATHER, max(reps, 8))
-    mg.set_x_device(x)
-    res["allgather_graph_ms_per_step"] = round(
-        spmv_dist.max_over_ranks(mg.run_graph(spmv_hw.MGPU_ALLGATHER, max(reps, 8)), dev), 5)
+    if square:
+        mg.set_x_device(x)
+        mg.run_graph(spmv_hw.MGPU_ALLGATHER, max(reps, 8))
+        mg.set_x_device(x)
+        res["allgather_graph_ms_per_step"] = round(
+            spmv_dist.max_over_ranks(mg.run_graph(spmv_hw.MGPU_ALLGATHER, max(reps, 8)), dev), 5)
     mg.destroy()
     return res
 
@@ -839,11 +846,14 @@ def distributed_parity(lib, args, world, rank, dev, y, st, held=None):
         y_full = spmv_dist.exchange_gather(y, counts)
         if held is not None:
             held["y_full"] = y_full  # rank 0: the assembled y (the dependent form's check)
-        res = {"scope": f"y of all {world} row slices gathered on rank 0 vs spmv_gold of the whole matrix",
+        res = {"scope": f"y of all {world} row slices gathered on rank 0 vs spmv_gold of the whole matrix"
+                        if not args.slice_of else f"rank 0's slice of a {args.slice_of}-way cut vs spmv_gold of its rows",
                "rows_checked": int(counts.sum())}
         if rank == 0:
             n, z = args.rows or 10_000_000, args.nnz or 160_000_000
-            rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+            r0 = held.get("row_begin", 0) if held is not None else 0  # (--slice-of: rank 0's slice)
+            rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4, row_begin=r0,
+                                                   row_end=r0 + int(counts.sum()))
             x = spmv_hw.gen_vector(lib, n, seed=6)
             err, nerr = check(rp, col, val, x, y_full)
             del rp, col, val, x
@@ -869,7 +879,8 @@ def serial_chain_ms(plan, x, y, steps, world, dev):
     before the next begins, as one spmv_hw call is one complete SpMV (csr_hw_wrapper.cpp:200-285).
     Replayed once untimed, then timed; max over ranks."""
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    # thread_local: a process-group watchdog thread polling its events does not void the capture
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(steps):
             plan.run(x, y)
     g.replay()
@@ -885,7 +896,7 @@ def serial_chain_ms(plan, x, y, steps, world, dev):
     return ms
 
 
-def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full):
+def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full, row0=0):
     """The dependent form (x <- A x): every step is this rank's SpMV into its
     slice and the all-gather of the slices into every rank's next x (spmv_dist.exchange_allgather),
     so step k + 1 cannot start before step k's exchange has ended. Timed over K steps from the
@@ -895,13 +906,14 @@ def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full):
     cnt[rank] = float(st["nr_rows"])
     counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
     nloc = int(st["nr_rows"])
+    total = int(counts.sum())
     ys = torch.empty(nloc, dtype=y.dtype, device=dev)
-    bufs = [x.clone(), torch.empty_like(x)]
+    bufs = [x.clone(), x.clone()]
 
-    def step(k):
+    def step(k):  # (row0 > 0 only for --slice-of: the gathered rows land at their own offset)
         src, dst = bufs[k % 2], bufs[(k + 1) % 2]
         plan.run(src, ys)
-        spmv_dist.exchange_allgather(ys, counts, out=dst)
+        spmv_dist.exchange_allgather(ys, counts, out=dst[row0:row0 + total])
 
     step(0)  # warm (communicator, staging buffers)
     bufs[0].copy_(x)
@@ -919,7 +931,8 @@ def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full):
     diff = 0.0
     if rank == 0 and y_full is not None:
         ref = y_full.to(dev).double()
-        diff = float(((bufs[1].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-300)).item())
+        diff = float(((bufs[1][row0:row0 + total].double() - ref).abs().max()
+                      / ref.abs().max().clamp_min(1e-300)).item())
     diff = spmv_dist.max_over_ranks(diff, dev)
     del bufs, ys
     return {"ms_per_step": round(ms, 5), "steps": steps,
@@ -1126,6 +1139,7 @@ def main():
         "n_ranks": dist.get_world_size() if dist.is_initialized() else 1,
         "launcher": os.environ.get("SPMV_BENCH_LAUNCHER") or ("torch.distributed.run" if world > 1 else None),
         "dist_rehearsal": bool(args.dist_rehearsal),
+        "slice_of": args.slice_of,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 5),
@@ -1173,7 +1187,7 @@ def main():
     # N > 1: parity is part of the measurement, not an extra (main.cpp:77-82 verifies every
     # spmv_hw result). It runs under the run deadline and the collective timeout only; a parity
     # that errors or fails prints the line with it and ends the run with status 3.
-    held = {}
+    held = {"row_begin": (desc.get("slice_rows") or [0])[0] if args.slice_of else 0}
     if os.environ.get("SPMV_BENCH_INJECT") == "parity" and rank == world - 1:
         y[0] += 1.0  # test hook (tests/test_gpu_bench.py): a wrong y must fail the run
     if args.multi:
@@ -1293,7 +1307,8 @@ def main():
     if args.multi and args.scaling == "strong" and args.workload == "powerlaw":
         # the dependent form x <- A x (square matrix): compute + all-gather in every step
         def dependent():
-            res = dependent_iteration(plan, x, y, st, args.steps, world, rank, dev, held.get("y_full"))
+            res = dependent_iteration(plan, x, y, st, args.steps, world, rank, dev, held.get("y_full"),
+                                      held.get("row_begin", 0))
             step_forms["dependent_ms_per_step"] = res["ms_per_step"]
             return res
         guarded("dependent", dependent)

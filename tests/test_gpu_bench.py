@@ -97,3 +97,22 @@ def test_bench_one_rank_rccl_rehearsal(scaling):
         sf = d["step_forms"]
         assert sf["dependent"]["pass"] and sf["dependent_ms_per_step"] > 0
         assert sf["dependent_native_graph_ms_per_step"] == nat["allgather_graph_ms_per_step"]
+
+
+def test_bench_rccl_rehearsal_of_a_split_slice():
+    """--dist-rehearsal --slice-of 4: the one RCCL rank holds rank 0's slice of a 4-way cut of the
+    400K-row matrix (a split sweep plan), so the line carries all three step forms over 'nccl':
+    the serial chain (value), the behind form of spmv_plan_run_graph and the dependent form, with
+    parity on the slice's rows and the dependent step checked against it."""
+    d = _bench("--dist-rehearsal", "--slice-of", "4", "--no-weak-companion")
+    assert d["slice_of"] == 4 and d["n_ranks"] == 1 and d["exchange"]["backend"] == "nccl"
+    r0, r1 = d["config"]["slice_rows"]
+    assert r0 == 0 and 0 < r1 < 400_000
+    p = d["parity"]
+    assert p["pass"] and p["rows_checked"] == r1 - r0
+    sf = d["step_forms"]
+    assert sf["value_form"] == "serial" and sf["serial_ms_per_step"] == d["ms_per_step"]
+    assert d["graph"]["run_graph_form"] == "behind" and sf["behind_ms_per_step"] > 0
+    assert sf["dependent"]["pass"] and sf["dependent_ms_per_step"] > 0
+    nat = d["exchange"]["native"]
+    assert "error" not in nat and nat["gather_compute_ms"] > 0, nat

@@ -55,6 +55,7 @@ for s in $STEPS; do
               SPMV_SWEEP_XCC_BIAS=0.02 run abbiasd_$i 400 python tools/strong_slices.py --ns 8,4 --slices all --graph-ab 20 --graph-modes product --rounds 3 --tag xcc_bias_0.02
             done ;;
     rccl1) run rccl1_strong 600 python bench.py --dist-rehearsal --scaling strong --no-weak-companion ;;
+    rccl1s8) run rccl1_slice8 600 python bench.py --dist-rehearsal --slice-of 8 --no-weak-companion ;;
     rehearse) SPMV_BENCH_BACKEND=gloo run rehearse_weak 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak
               SPMV_BENCH_BACKEND=gloo run rehearse_strong 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --scaling strong ;;
     ab) run ab 600 python tools/ab_variants.py ;;
