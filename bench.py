@@ -124,7 +124,9 @@ def parse(argv=None):
     if a.slice_of is not None and not (a.dist_rehearsal and a.slice_of >= 1):
         ap.error("--slice-of N needs --dist-rehearsal (and N >= 1)")
     if a.scaling is None:
-        a.scaling = "strong" if a.gpus > 1 else "weak"
+        a.scaling = "strong" if a.gpus > 1 or a.slice_of else "weak"
+    if a.slice_of and a.scaling != "strong":
+        ap.error("--slice-of is a slice of the strong-scaling cut")
     a.multi = a.gpus > 1 or a.dist_rehearsal  # the N > 1 path: a process group, slices, exchange
     return a
 
