@@ -100,14 +100,17 @@ def test_bench_one_rank_rccl_rehearsal(scaling):
 
 
 def test_bench_rccl_rehearsal_of_a_split_slice():
-    """--dist-rehearsal --slice-of 4: the one RCCL rank holds rank 0's slice of a 4-way cut of the
-    400K-row matrix (a split sweep plan), so the line carries all three step forms over 'nccl':
-    the serial chain (value), the behind form of spmv_plan_run_graph and the dependent form, with
-    parity on the slice's rows and the dependent step checked against it."""
-    d = _bench("--dist-rehearsal", "--slice-of", "4", "--no-weak-companion")
+    """--dist-rehearsal --slice-of 4: the one RCCL rank holds rank 0's slice of a 4-way cut of a
+    4M-row / 64M-nnz power-law matrix (~1M rows: a split sweep plan, like an 8-GPU rank's slice
+    of the 10M/160M matrix), so the line carries all three step forms over 'nccl': the serial
+    chain (value, a torch graph captured with the process group up), the behind form of
+    spmv_plan_run_graph and the dependent form, with parity on the slice's rows and the
+    dependent step checked against it."""
+    d = _bench("--dist-rehearsal", "--slice-of", "4", "--no-weak-companion", "--rows", "4000000",
+               "--nnz", "64000000")
     assert d["slice_of"] == 4 and d["n_ranks"] == 1 and d["exchange"]["backend"] == "nccl"
     r0, r1 = d["config"]["slice_rows"]
-    assert r0 == 0 and 0 < r1 < 400_000
+    assert r0 == 0 and 900_000 < r1 < 1_100_000
     p = d["parity"]
     assert p["pass"] and p["rows_checked"] == r1 - r0
     sf = d["step_forms"]
