@@ -903,7 +903,8 @@ def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full, row0=0)
     slice and the all-gather of the slices into every rank's next x (spmv_dist.exchange_allgather),
     so step k + 1 cannot start before step k's exchange has ended. Timed over K steps from the
     headline's x, max over ranks. Checked: one step from that x gives, on every rank, the y the
-    parity gather assembled on rank 0 (within 1e-12 relative: the LDS adds' order)."""
+    parity gather assembled on rank 0 (within 1e-12 relative in fp64, 1e-5 in fp32: the LDS adds'
+    order)."""
     cnt = [0.0] * world
     cnt[rank] = float(st["nr_rows"])
     counts = np.array(spmv_dist.sum_over_ranks(cnt, dev), dtype=np.int64)
@@ -936,10 +937,11 @@ def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full, row0=0)
         diff = float(((bufs[1][row0:row0 + total].double() - ref).abs().max()
                       / ref.abs().max().clamp_min(1e-300)).item())
     diff = spmv_dist.max_over_ranks(diff, dev)
+    tol = 1e-12 if y.element_size() == 8 else 1e-5  # two runs of the sweep differ in the LDS adds' order
     del bufs, ys
     return {"ms_per_step": round(ms, 5), "steps": steps,
             "form": "SpMV into the rank's slice, then all-gather of the slices into every rank's next x",
-            "x1_max_rel_diff_vs_parity_y": diff, "pass": bool(diff <= 1e-12)}
+            "x1_max_rel_diff_vs_parity_y": diff, "tol": tol, "pass": bool(diff <= tol)}
 
 
 def main():
