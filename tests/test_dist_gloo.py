@@ -61,6 +61,21 @@ def _worker(rank, world, port, mode, q):
                 yb[:r1 - r0] = torch.from_numpy(oracle.spmv_gold(*sub, x * (k + 1)))
 
             full = sdist.pipelined_gather(step, bufs, counts, 5)
+        elif mode == "dependent":
+            # bench.py's dependent form (x <- A x): each rank's slice of A x_k, all-gathered into a
+            # preallocated next-x buffer (a view, as bench passes it), three steps
+            counts = sdist.slice_counts(bounds)
+            sub = ((rp - rp[0]).astype(np.uint32), col[rp[0]:rp[-1]], val[rp[0]:rp[-1]])
+            bufs = [torch.from_numpy(x.copy()), torch.zeros(n + 7, dtype=torch.float64)]
+            for k in range(3):
+                src, dst = bufs[k % 2], bufs[(k + 1) % 2]
+                ys = torch.from_numpy(oracle.spmv_gold(*sub, src[:n].numpy()))
+                sdist.exchange_allgather(ys, counts, out=dst[:n])
+            full = bufs[1][:n]
+            ref = x
+            for _ in range(3):
+                ref = oracle.spmv_gold(row_ptr, col, val, ref)
+            assert np.array_equal(full.numpy(), ref)  # every rank holds A^3 x
         elif mode == "reduce":
             full = sdist.exchange_reduce(y_t, r0, n)
         elif mode == "gather":
@@ -73,16 +88,19 @@ def _worker(rank, world, port, mode, q):
         assert np.array_equal(xb.numpy(), x)
         m = sdist.max_over_ranks(float(rank), torch.device("cpu"))
         if rank == 0:
-            y_ref = oracle.spmv_gold(row_ptr, col, val, x * 5 if mode == "pipelined" else x)  # last step: x * 5
+            if mode == "dependent":
+                y_ref = ref
+            else:
+                y_ref = oracle.spmv_gold(row_ptr, col, val, x * 5 if mode == "pipelined" else x)  # last step: x * 5
             q.put((np.array_equal(full.numpy(), y_ref), m, list(sdist.slice_counts(bounds))))
-        elif mode != "allgather":
+        elif mode not in ("allgather", "dependent"):
             assert full is None
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("mode", ["reduce", "gather", "allgather", "pipelined"])
+@pytest.mark.parametrize("mode", ["reduce", "gather", "allgather", "pipelined", "dependent"])
 def test_row_sliced_exchange_rebuilds_y(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
