@@ -973,6 +973,8 @@ def main():
     torch.cuda.synchronize()
 
     stage("timed")
+    if os.environ.get("SPMV_BENCH_INJECT") == "hang" and rank == world - 1:
+        time.sleep(3600)  # test hook (tests/test_gpu_bench.py): a rank that never reaches the barrier
     # 1) eager: one host launch per step, the main kernel timed with HIP events on its stream
     #    (roofline.achieved; rocprofv3 sees the same launches)
     barrier(world)

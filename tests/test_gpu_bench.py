@@ -119,3 +119,18 @@ def test_bench_rccl_rehearsal_of_a_split_slice():
     assert sf["dependent"]["pass"] and sf["dependent_ms_per_step"] > 0
     nat = d["exchange"]["native"]
     assert "error" not in nat and nat["gather_compute_ms"] > 0, nat
+
+
+def test_bench_hung_rank_ends_at_the_run_timeout():
+    """VERDICT r4 item 1 on the GPU: rank 1 never reaches the timed region's barrier (test hook
+    SPMV_BENCH_INJECT=hang), so rank 0 waits in the collective. The self-launch parent kills both
+    at --run-timeout, prints one error line naming each rank's stage ("timed") and exits 124."""
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    e.update(SPMV_BENCH_BACKEND="gloo", SPMV_BENCH_INJECT="hang")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--gpus", "2", "--run-timeout", "75"],
+                       capture_output=True, text=True, env=e, cwd=ROOT, timeout=110)
+    assert p.returncode == 124, p.stdout[-2000:] + p.stderr[-3000:]
+    (line,) = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert line["value"] is None and "run timeout" in line["error"]
+    assert line["stage"] == {"0": "timed", "1": "timed"}, line
