@@ -75,6 +75,17 @@ def test_self_launch_rank0_done_others_hung():
     assert "killed as hung" in p.stderr
 
 
+def test_self_launch_teardown_hang_after_the_line_is_not_a_failure():
+    """A rank that finished (past its line, parity included) but hangs in teardown is killed after
+    --spawn-grace; the run keeps status 0, since the measurement is complete."""
+    p = _run("--gpus", "3", "--dry-launch", "--dry-launch-rc", "1:teardown-hang", "--spawn-grace", "1", timeout=60)
+    assert p.returncode == 0, (p.returncode, p.stderr)
+    assert "teardown hang" in p.stderr
+    p = _run("--gpus", "3", "--dry-launch", "--dry-launch-rc", "1:teardown-hang,2:hang", "--spawn-grace", "1",
+             timeout=60)
+    assert p.returncode == 137, (p.returncode, p.stderr)  # rank 2 never finished
+
+
 def test_self_launch_failed_rank0_gets_an_error_line():
     """Rank 0 failed before printing its line: the parent prints the error line (stages, statuses)."""
     p = _run("--gpus", "2", "--dry-launch", "--dry-launch-rc", "0:5", timeout=60)
