@@ -1358,6 +1358,11 @@ def main():
     if isinstance(par, dict) and par.get("pass") is False:  # N = 1: the full-size check failed
         print(f"bench.py: parity did not pass: {par}", file=sys.stderr, flush=True)
         os._exit(3)
+    # the line is out and verified: a teardown that hangs (plan or process-group destruction) must
+    # not hold the run (under torch.distributed.run no parent would end it before --run-timeout)
+    teardown = threading.Timer(args.spawn_grace, lambda: os._exit(0))
+    teardown.daemon = True
+    teardown.start()
     plan.destroy()
     if dist.is_initialized():
         dist.destroy_process_group()
