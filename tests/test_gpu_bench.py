@@ -128,7 +128,7 @@ def test_bench_hung_rank_ends_at_the_run_timeout():
     e = {k: v for k, v in os.environ.items()
          if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     e.update(SPMV_BENCH_BACKEND="gloo", SPMV_BENCH_INJECT="hang")
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--gpus", "2", "--run-timeout", "75"],
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--gpus", "2", "--run-timeout", "40"],
                        capture_output=True, text=True, env=e, cwd=ROOT, timeout=110)
     assert p.returncode == 124, p.stdout[-2000:] + p.stderr[-3000:]
     (line,) = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
