@@ -119,3 +119,42 @@ def test_config3_deterministic_sweep_bitwise_over_runs(monkeypatch):
     h_val, h_x, h_y = val.cpu().numpy(), x.cpu().numpy(), y0.cpu().numpy()
     ref = oracle.spmv_gold(h_rp, h_col, h_val, h_x)
     assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, h_y) <= 1e-12
+
+
+@pytest.mark.timeout(900)
+def test_config4_through_the_dropin_with_8_units(monkeypatch):
+    """Config 4 the reference's own way: the 10M/160M matrix through Part 1 (create_csr_hw_matrix
+    / spmv_hw, csr_hw_wrapper.cpp:3-80, :193-288) with 8 units ("ComputeUnits", here virtual
+    units sharing the box's GPU), each holding its nnz-balanced row slice (csr_hw.cpp:459-468, the
+    cut bench.py --gpus 8 makes), and the host merge of the slices into the caller's y
+    (accum_results' +=, csr_hw.cpp:1531-1565). y matches spmv_gold of the whole matrix, the
+    reference's verification (abs 1e-5) passes, a second call adds A x once more, and every
+    unit's slice is the 8-way strong-scaling cut."""
+    monkeypatch.setenv("SPMV_NGPUS", "8")
+    monkeypatch.setenv("SPMV_HW_MERGE", "host")
+    lib = spmv_hw.load(np.float64)
+    n, z = 10_000_000, 160_000_000
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    h_rp, h_col = rp.cpu().numpy().view(np.uint32), col.cpu().numpy().view(np.uint32)
+    h_val, h_x = val.cpu().numpy(), x.cpu().numpy()
+    del rp, col, val, x
+    m = lib.make_csr_matrix(h_rp, h_col, h_val, n)
+    hw, bm = lib.create_csr_hw_matrix(m)
+    bounds = lib.partition_rows(h_rp, 8)
+    for u in range(8):  # the units' slices: the strong-scaling cut, row for row
+        assert hw[u].contents.nr_rows[0] == bounds[u + 1] - bounds[u]
+        assert hw[u].contents.nr_nzeros[0] == h_rp[bounds[u + 1]] - h_rp[bounds[u]]
+    hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(h_x), 1, hw[0].contents.nr_cols)
+    yv = lib.make_csr_vector(np.zeros(n))
+    lib.spmv_hw(hw, hx, yv, bm)
+    y1 = np.ctypeslib.as_array(yv.values, shape=(n,)).copy()
+    lib.spmv_hw(hw, hx, yv, bm)
+    y2 = np.ctypeslib.as_array(yv.values, shape=(n,)).copy()
+    lib.delete_csr_hw_matrix(hw)
+    lib.free_bitmap(bm)
+    lib.delete_csr_hw_x_vector(hx)
+    ref = oracle.spmv_gold(h_rp, h_col, h_val, h_x)
+    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y1) <= 1e-12
+    assert lib.verification(ref, y1) == 0
+    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y2 - y1) <= 1e-12
