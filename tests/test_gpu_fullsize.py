@@ -142,9 +142,12 @@ def test_config4_through_the_dropin_with_8_units(monkeypatch):
     m = lib.make_csr_matrix(h_rp, h_col, h_val, n)
     hw, bm = lib.create_csr_hw_matrix(m)
     bounds = lib.partition_rows(h_rp, 8)
-    for u in range(8):  # the units' slices: the strong-scaling cut, row for row
+    for u in range(8):  # the units' slices: the strong-scaling cut, row for row (every row is
+        # non-empty here, so the compact row count is the slice's); nr_nzeros counts the stored,
+        # chunk-padded entries of the unit's representation
         assert hw[u].contents.nr_rows[0] == bounds[u + 1] - bounds[u]
-        assert hw[u].contents.nr_nzeros[0] == h_rp[bounds[u + 1]] - h_rp[bounds[u]]
+        z_u = int(h_rp[bounds[u + 1]]) - int(h_rp[bounds[u]])
+        assert z_u <= hw[u].contents.nr_nzeros[0] <= 1.01 * z_u
     hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(h_x), 1, hw[0].contents.nr_cols)
     yv = lib.make_csr_vector(np.zeros(n))
     lib.spmv_hw(hw, hx, yv, bm)
