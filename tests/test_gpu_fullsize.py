@@ -122,7 +122,8 @@ def test_config3_deterministic_sweep_bitwise_over_runs(monkeypatch):
 
 
 @pytest.mark.timeout(900)
-def test_config4_through_the_dropin_with_8_units(monkeypatch):
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_config4_through_the_dropin_with_8_units(monkeypatch, dtype):
     """Config 4 the reference's own way: the 10M/160M matrix through Part 1 (create_csr_hw_matrix
     / spmv_hw, csr_hw_wrapper.cpp:3-80, :193-288) with 8 units ("ComputeUnits", here virtual
     units sharing the box's GPU), each holding its nnz-balanced row slice (csr_hw.cpp:459-468, the
@@ -132,7 +133,7 @@ def test_config4_through_the_dropin_with_8_units(monkeypatch):
     unit's slice is the 8-way strong-scaling cut."""
     monkeypatch.setenv("SPMV_NGPUS", "8")
     monkeypatch.setenv("SPMV_HW_MERGE", "host")
-    lib = spmv_hw.load(np.float64)
+    lib = spmv_hw.load(dtype)
     n, z = 10_000_000, 160_000_000
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=4)
     x = spmv_hw.gen_vector(lib, n, seed=6)
@@ -149,7 +150,7 @@ def test_config4_through_the_dropin_with_8_units(monkeypatch):
         z_u = int(h_rp[bounds[u + 1]]) - int(h_rp[bounds[u]])
         assert z_u <= hw[u].contents.nr_nzeros[0] <= 1.01 * z_u
     hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(h_x), 1, hw[0].contents.nr_cols)
-    yv = lib.make_csr_vector(np.zeros(n))
+    yv = lib.make_csr_vector(np.zeros(n, dtype))
     lib.spmv_hw(hw, hx, yv, bm)
     y1 = np.ctypeslib.as_array(yv.values, shape=(n,)).copy()
     lib.spmv_hw(hw, hx, yv, bm)
@@ -158,6 +159,14 @@ def test_config4_through_the_dropin_with_8_units(monkeypatch):
     lib.free_bitmap(bm)
     lib.delete_csr_hw_x_vector(hx)
     ref = oracle.spmv_gold(h_rp, h_col, h_val, h_x)
-    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y1) <= 1e-12
-    assert lib.verification(ref, y1) == 0
-    assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y2 - y1) <= 1e-12
+    if np.dtype(dtype) == np.float64:
+        assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y1) <= 1e-12
+        assert lib.verification(ref, y1) == 0
+        assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y2 - y1) <= 1e-12
+    else:  # fp32: the north-star gate against spmv_gold, the tight bound against fp64 sums
+        assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref, y1) <= TOL[np.dtype(np.float32)]
+        ref64 = oracle.spmv_fp64acc(h_rp, h_col, h_val, h_x)
+        assert oracle.scaled_error(h_rp, h_col, h_val, h_x, ref64, y1) <= FP32_TIGHT
+        # the second call's y is y1 + A x rounded in fp32 (the += happens in fp32 on the host)
+        assert oracle.scaled_error(h_rp, h_col, h_val, h_x, 2 * ref64.astype(np.float64),
+                                   y2.astype(np.float64)) <= 4 * FP32_TIGHT
