@@ -129,3 +129,14 @@ def test_dist_rehearsal_is_one_gpu_only():
     assert p.returncode == 2 and "one-GPU form" in p.stderr, p.stderr
     p = _run("--dist-rehearsal", "--dry-launch")
     assert p.returncode == 0, p.stderr
+
+
+def test_slice_of_needs_the_rehearsal_and_the_strong_cut():
+    """--slice-of N is the one-rank RCCL rehearsal of an N-GPU rank's slice: refused without
+    --dist-rehearsal and with --scaling weak (argparse status 2); accepted with both."""
+    p = _run("--slice-of", "8", "--dry-launch")
+    assert p.returncode == 2 and "--dist-rehearsal" in p.stderr
+    p = _run("--dist-rehearsal", "--slice-of", "8", "--scaling", "weak", "--dry-launch")
+    assert p.returncode == 2 and "strong-scaling cut" in p.stderr
+    p = _run("--dist-rehearsal", "--slice-of", "8", "--dry-launch")
+    assert p.returncode == 0, p.stderr
