@@ -74,9 +74,10 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="default: strong (config 4) when --gpus > 1, weak (= single GPU) otherwise")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
-    ap.add_argument("--extras-timeout", type=float, default=420.0,
+    ap.add_argument("--extras-timeout", type=float, default=None,
                     help="seconds the reported-only fields after the measurement may take before the "
-                         "line is printed without them")
+                         "line is printed without them (default 420 at N = 1, where the CPU baseline runs, "
+                         "240 at N > 1)")
     ap.add_argument("--extras-timeout-status", type=int, default=0,
                     help="exit status after the watchdog printed the line (the line stays valid: it "
                          "carries `extras_timeout`, and at N > 1 its parity already passed; set e.g. 3 to "
@@ -129,6 +130,8 @@ def parse(argv=None):
     if a.slice_of and a.scaling != "strong":
         ap.error("--slice-of is a slice of the strong-scaling cut")
     a.multi = a.gpus > 1 or a.dist_rehearsal  # the N > 1 path: a process group, slices, exchange
+    if a.extras_timeout is None:
+        a.extras_timeout = 240.0 if a.multi else 420.0
     return a
 
 
