@@ -60,6 +60,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spmv-fpga_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+DRIVER_LIMIT_S = 600.0  # the driver's limit on one bench run (BENCH_r05.json run.timeout_s)
+RUN_TIMEOUT_DEFAULT = 480.0  # the run's own deadline: below DRIVER_LIMIT_S with --spawn-grace to spare
 
 
 def parse(argv=None):
@@ -73,11 +75,16 @@ def parse(argv=None):
     ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="default: strong (config 4) when --gpus > 1, weak (= single GPU) otherwise")
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / full-size parity")
+    ap.add_argument("--no-cpu", action="store_true",
+                    help="skip the CPU baseline timing (the full-size parity check always runs)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in boundary measurement (create_csr_hw_matrix -> spmv_hw -> "
+                         "verification in a child process, the reference's run.elf timings)")
+    ap.add_argument("--dropin-reps", type=int, default=5, help="spmv_hw calls of the drop-in measurement")
     ap.add_argument("--extras-timeout", type=float, default=None,
-                    help="seconds the reported-only fields after the measurement may take before the "
-                         "line is printed without them (default 420 at N = 1, where the CPU baseline runs, "
-                         "240 at N > 1)")
+                    help="seconds the reported-only fields after the verified measurement may take before "
+                         "the line is printed without them (default: half the run timeout at N = 1, 3/8 of "
+                         "it at N > 1)")
     ap.add_argument("--extras-timeout-status", type=int, default=0,
                     help="exit status after the watchdog printed the line (the line stays valid: it "
                          "carries `extras_timeout`, and at N > 1 its parity already passed; set e.g. 3 to "
@@ -107,13 +114,16 @@ def parse(argv=None):
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
     ap.add_argument("--spawn-grace", type=float, default=60.0,
-                    help="self-launch: seconds the other ranks may run on after one rank exited (with any "
-                         "status); ranks still running then are hung, killed, and the run fails")
-    ap.add_argument("--run-timeout", type=float, default=900.0,
-                    help="seconds the whole run may take (below the driver's limit): then every rank is "
-                         "killed and one JSON error line names each rank's last stage; exit status 124")
-    ap.add_argument("--collective-timeout", type=float, default=300.0,
-                    help="N > 1: timeout of every torch.distributed collective (init_process_group)")
+                    help="self-launch: seconds the other ranks may run on after one rank failed (non-zero "
+                         "status), or after a rank finished cleanly (for rank 0 only once it printed its "
+                         "line: it alone does work after the last collective); ranks still running then "
+                         "are hung, killed, and the run fails")
+    ap.add_argument("--run-timeout", type=float, default=RUN_TIMEOUT_DEFAULT,
+                    help="seconds the whole run may take (below the driver's 600 s limit): then every rank "
+                         "is killed and one JSON error line names each rank's last stage; exit status 124")
+    ap.add_argument("--collective-timeout", type=float, default=None,
+                    help="N > 1: timeout of every torch.distributed collective (init_process_group; "
+                         "default min(120, run timeout / 4))")
     ap.add_argument("--dry-launch", action="store_true",
                     help="every rank prints its launch environment as JSON and exits before any GPU call")
     ap.add_argument("--dry-launch-rc", default="",
@@ -130,8 +140,14 @@ def parse(argv=None):
     if a.slice_of and a.scaling != "strong":
         ap.error("--slice-of is a slice of the strong-scaling cut")
     a.multi = a.gpus > 1 or a.dist_rehearsal  # the N > 1 path: a process group, slices, exchange
+    # every deadline derives from --run-timeout, which stays below the driver's limit (VERDICT r5
+    # item 2): a run that reaches its extras by run/2 (N = 1) or 5/8 of it (N > 1) still prints
+    # its line from the extras watchdog before the run deadline, and a hung collective gives up
+    # well before either
     if a.extras_timeout is None:
-        a.extras_timeout = 240.0 if a.multi else 420.0
+        a.extras_timeout = a.run_timeout * (0.375 if a.multi else 0.5)
+    if a.collective_timeout is None:
+        a.collective_timeout = min(120.0, a.run_timeout / 4)
     return a
 
 
@@ -208,6 +224,7 @@ def spawn_ranks(args, argv):
     for sig in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sig, stop)
     stages = {r: "launched" for r in range(n)}
+    finished_at = {}  # rank -> when it reached "emitted" / "done" (its line is out; teardown only)
     pending = b""
 
     def read_stages():
@@ -225,15 +242,36 @@ def spawn_ranks(args, argv):
                 rank, _, st = ln.decode(errors="replace").partition(":")
                 if rank.isdigit() and int(rank) in stages:
                     stages[int(rank)] = st
+                    if st in ("emitted", "done"):
+                        finished_at.setdefault(int(rank), time.monotonic())
+
+    def grace_start(r, failed_at, clean_at):
+        """When rank r's --spawn-grace starts: at the first failed rank; after a clean exit, at
+        once for ranks > 0 (rank 0 still owes the line, the others only the collectives rank 0
+        has passed), but for rank 0 only once it printed its line -- it alone does work after
+        the last collective (the drop-in child, the CPU baseline), bounded by the run deadline."""
+        if failed_at is not None:
+            return failed_at
+        if clean_at is None:
+            return None
+        if r != 0:
+            return clean_at
+        return max(clean_at, finished_at[0]) if 0 in finished_at else None
 
     t0 = time.monotonic()
-    first_exit, error, hung = None, None, []
+    failed_at, clean_at, error, hung = None, None, None, []
     while any(p.poll() is None for p in procs):
         read_stages()
         now = time.monotonic()
-        if first_exit is None and any(p.poll() is not None for p in procs):
-            first_exit = now
-        if now - t0 > args.run_timeout or (first_exit is not None and now - first_exit > args.spawn_grace):
+        for p in procs:
+            rc = p.poll()
+            if rc is not None and rc != 0 and failed_at is None:
+                failed_at = now
+            if rc == 0 and clean_at is None:
+                clean_at = now
+        late = [r for r, p in enumerate(procs) if p.poll() is None
+                and (grace_start(r, failed_at, clean_at) or now) + args.spawn_grace < now]
+        if now - t0 > args.run_timeout or late:
             read_stages()
             hung = [r for r, p in enumerate(procs) if p.poll() is None]
             error = (f"run timeout: ranks {hung} still running after {args.run_timeout:g} s, killed"
@@ -270,7 +308,9 @@ def dry_launch(args):
     env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
                                           "MASTER_ADDR", "MASTER_PORT", "SPMV_BENCH_LAUNCHER")}
     rank = int(os.environ.get("RANK", "0"))
-    print(json.dumps({"dry_launch": True, "gpus": args.gpus, "pid": os.getpid(), **env}), flush=True)
+    deadlines = {k: getattr(args, k) for k in ("run_timeout", "extras_timeout", "collective_timeout", "spawn_grace")}
+    print(json.dumps({"dry_launch": True, "gpus": args.gpus, "pid": os.getpid(), "deadlines": deadlines,
+                      "driver_limit_s": DRIVER_LIMIT_S, **env}), flush=True)
     codes = dict(kv.split(":") for kv in args.dry_launch_rc.split(",") if kv)
     code = codes.get(str(rank), "0")
     stage("init")
@@ -287,6 +327,15 @@ def dry_launch(args):
 
 
 _STAGE = ["start"]
+_CHILDREN = []  # child processes of this rank (the drop-in run), ended with it
+
+
+def _kill_children():
+    for p in list(_CHILDREN):
+        try:
+            p.kill()
+        except OSError:
+            pass
 
 
 def stage(name):
@@ -313,6 +362,7 @@ def arm_run_watchdog(args):
         if int(os.environ.get("RANK", "0")) == 0 and _STAGE[0] != "emitted":
             print(error_line(args, f"run timeout after {args.run_timeout:g} s", {0: _STAGE[0]}, 124), flush=True)
         sys.stdout.flush()
+        _kill_children()
         os._exit(124)
 
     t = threading.Timer(args.run_timeout, expire)
@@ -398,27 +448,57 @@ def build_workload(lib, args, world, rank):
     return rp, col, val, x, n, desc
 
 
-def cpu_baseline(lib, rp, col, val, x, y_gpu, reps, args_threads=16):
-    """Times the oracle's restatement of spmv_gold (1 thread, -O2 -ffp-contract=off) on the
-    same matrix in host memory, and checks the full-size GPU result against it."""
+def host_csr(rp, col, val, x, y):
+    """The measured matrix, x and the GPU's y in host memory (numpy), for the checks after the
+    timed region."""
+    return {"rp": rp.cpu().numpy().view(np.uint32), "col": col.cpu().numpy().view(np.uint32),
+            "val": val.cpu().numpy(), "x": x.cpu().numpy(), "y": y.cpu().numpy()}
+
+
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    return oracle
 
-    h_rp = rp.cpu().numpy().view(np.uint32)
-    h_col = col.cpu().numpy().view(np.uint32)
-    h_val = val.cpu().numpy()
-    h_x = x.cpu().numpy()
-    n = len(h_rp) - 1
-    y = np.zeros(n, h_val.dtype)
+
+def full_parity(h):
+    """N = 1: the measured y against the oracle's restatement of spmv_gold (csr.cpp:184-194) on the
+    whole matrix -- the check main.cpp:77-82 makes after every spmv_hw. Part of the measurement,
+    not an extra: it runs before the extras watchdog, and a failed or missing check fails the
+    run (status 3). Returns (parity, the oracle's y, its 1-thread time in ms)."""
+    oracle = _oracle()
+    n = len(h["rp"]) - 1
+    ref = np.zeros(n, h["val"].dtype)
+    t0 = time.perf_counter()
+    oracle.spmv_gold_rows(h["rp"], h["col"], h["val"], h["x"], 0, n, out=ref)
+    sw_ms = (time.perf_counter() - t0) * 1e3
+    yg = h["y"]
+    err = oracle.scaled_error(h["rp"], h["col"], h["val"], h["x"], ref, yg)
+    abs_errors = oracle.verification_errors(ref, yg.astype(ref.dtype))
+    yr, yg64 = ref.astype(np.float64), yg.astype(np.float64)
+    nz = yr != 0
+    rel = float(np.max(np.abs(yg64[nz] - yr[nz]) / np.abs(yr[nz]))) if nz.any() else 0.0
+    tol = 1e-6 if ref.dtype == np.float64 else 1e-4
+    parity = {"scope": f"full matrix ({n} rows) vs spmv_gold", "rows_checked": n, "max_scaled_err": err, "tol": tol,
+              "max_rel_err": rel, "ref_abs_1e-5_errors": abs_errors,
+              "pass": bool(err <= tol and abs_errors == 0)}
+    return parity, ref, sw_ms
+
+
+def cpu_baseline(lib, h, ref, reps, args_threads=16):
+    """Times the oracle's restatement of spmv_gold (1 thread, -O2 -ffp-contract=off) on the
+    same matrix in host memory; every run must give the parity check's y bit for bit."""
+    oracle = _oracle()
+    n = len(h["rp"]) - 1
+    y = np.zeros(n, h["val"].dtype)
     times = []
     for _ in range(max(1, reps)):
         t0 = time.perf_counter()
-        oracle.spmv_gold_rows(h_rp, h_col, h_val, h_x, 0, n, out=y)
+        oracle.spmv_gold_rows(h["rp"], h["col"], h["val"], h["x"], 0, n, out=y)
         times.append(time.perf_counter() - t0)
+    assert np.array_equal(y.view(np.uint8), ref.view(np.uint8))
     t = float(np.median(times))
-    nnz = int(h_rp[-1])
-    err = oracle.scaled_error(h_rp, h_col, h_val, h_x, y, y_gpu.cpu().numpy())
-    abs_errors = oracle.verification_errors(y, y_gpu.cpu().numpy().astype(h_val.dtype))
+    nnz = int(h["rp"][-1])
     try:
         model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
     except Exception:
@@ -431,13 +511,13 @@ def cpu_baseline(lib, rp, col, val, x, y_gpu, reps, args_threads=16):
     # releases the GIL; nnz-balanced row slices), labelled as such
     from concurrent.futures import ThreadPoolExecutor
     nt = max(1, min(args_threads, os.cpu_count() or 1))
-    bounds = lib.partition_rows(h_rp, nt)
-    y_mt = np.zeros(n, h_val.dtype)
+    bounds = lib.partition_rows(h["rp"], nt)
+    y_mt = np.zeros(n, h["val"].dtype)
 
     def part(t):
         r0, r1 = int(bounds[t]), int(bounds[t + 1])
         if r1 > r0:
-            oracle.spmv_gold_rows(h_rp, h_col, h_val, h_x, r0, r1, out=y_mt[r0:r1])
+            oracle.spmv_gold_rows(h["rp"], h["col"], h["val"], h["x"], r0, r1, out=y_mt[r0:r1])
 
     times_mt = []
     with ThreadPoolExecutor(nt) as ex:
@@ -446,19 +526,96 @@ def cpu_baseline(lib, rp, col, val, x, y_gpu, reps, args_threads=16):
             list(ex.map(part, range(nt)))
             times_mt.append(time.perf_counter() - t0)
     t_mt = float(np.median(times_mt))
-    assert np.array_equal(y_mt.view(np.uint8), y.view(np.uint8))  # same rows, same order
+    assert np.array_equal(y_mt.view(np.uint8), ref.view(np.uint8))  # same rows, same order
     base["threads_line"] = {"value": round(2.0 * nnz / t_mt / 1e9, 4), "unit": "GFLOP/s", "cores": nt,
                             "kind": "port", "sample": f"same matrix, row-parallel restatement: {nt} threads "
                                                       f"over nnz-balanced row slices, median of {len(times_mt)} "
                                                       f"runs, {t_mt * 1e3:.1f} ms/SpMV"}
-    yg = y_gpu.cpu().numpy().astype(np.float64)
-    yr = y.astype(np.float64)
-    nz = yr != 0
-    rel = float(np.max(np.abs(yg[nz] - yr[nz]) / np.abs(yr[nz]))) if nz.any() else 0.0
-    parity = {"max_scaled_err": err, "tol": 1e-6 if h_val.dtype == np.float64 else 1e-4,
-              "max_rel_err": rel, "ref_abs_1e-5_errors": abs_errors,
-              "pass": bool(err <= (1e-6 if h_val.dtype == np.float64 else 1e-4))}
-    return base, parity
+    return base
+
+
+def _ref_lines(text, prefix):
+    """The values of the reference's timing lines "<prefix> : <ms> ms elapsed" (csr_hw_wrapper.cpp:
+    274,284-285, main.cpp:72) in the order printed."""
+    out = []
+    for ln in text.splitlines():
+        if ln.startswith(prefix):
+            try:
+                out.append(float(ln.split(":", 1)[1].split()[0]))
+            except (IndexError, ValueError):
+                pass
+    return out
+
+
+def run_dropin(args, units, merge, ref, sw_ms, timeout):
+    """The drop-in boundary itself: the reference's run.elf flow -- the host
+    CSR through create_csr_hw_matrix + create_csr_hw_x_vector ("Matrix read time", main.cpp:67-72),
+    spmv_hw ("Hardware execution time", "Result accumulation time", "Total time",
+    csr_hw_wrapper.cpp:272-285) and verification against spmv_gold's y (main.cpp:77-82) -- in a
+    child process (spmv-fpga_amd/dropin_main.py) on the same synthetic matrix, `units` units
+    ("ComputeUnits", one per GPU) merged by `merge`. The first call's times are the reference's
+    single-run numbers; the median over --dropin-reps calls is beside them. Every call is
+    verified; `pass` is false when any call's verification is not 0."""
+    import tempfile
+    n = ref.shape[0]
+    z = (args.nnz or 160_000_000) if args.workload == "powerlaw" else 16 * n
+    fd, path = tempfile.mkstemp(suffix=".npy", prefix="spmv_dropin_ref_")
+    os.close(fd)
+    t0 = time.perf_counter()
+    try:
+        np.save(path, ref)
+        cmd = [sys.executable, os.path.join(ROOT, "spmv-fpga_amd", "dropin_main.py"), "--workload", args.workload,
+               "--dtype", args.dtype, "--rows", str(n), "--nnz", str(z), "--units", str(units), "--merge", merge,
+               "--reps", str(max(1, args.dropin_reps)), "--ref", path]
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR",
+                            "MASTER_PORT", STAGE_FD_ENV, "SPMV_NGPUS", "SPMV_HW_MERGE")}
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT)
+        _CHILDREN.append(p)  # killed by the watchdogs if the run ends while it works
+        try:
+            out, err = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.communicate()
+            return {"error": f"drop-in child still running after {timeout:g} s, killed", "pass": None}
+        finally:
+            _CHILDREN.remove(p)
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+    js = [ln[len("DROPIN_JSON "):] for ln in out.splitlines() if ln.startswith("DROPIN_JSON ")]
+    if p.returncode not in (0, 3) or not js:
+        return {"error": f"drop-in child exit status {p.returncode}: {(err or out)[-400:]}", "pass": None}
+    d = json.loads(js[-1])
+    hw = _ref_lines(out, "Hardware execution time")
+    ra = _ref_lines(out, "Result accumulation time")
+    tot = _ref_lines(out, "Total time")
+    calls = d["calls"]
+    if not (len(hw) == len(ra) == len(tot) == len(calls) >= 1):
+        return {"error": f"drop-in child printed {len(hw)}/{len(ra)}/{len(tot)} timing lines for "
+                         f"{len(calls)} spmv_hw calls", "pass": None}
+    tol = 1e-6 if args.dtype == "f64" else 1e-4
+    med = lambda v: round(float(np.median(v)), 4)  # noqa: E731
+    res = {"api": "create_csr_hw_matrix + create_csr_hw_x_vector -> spmv_hw -> verification "
+                  "(main.cpp:67-82 over the Part-1 C-ABI, child process spmv-fpga_amd/dropin_main.py)",
+           "units": d["units"], "merge": merge, "rows": d["rows"], "nnz": d["nnz"],
+           "matrix_read_ms": d["matrix_read_ms"],
+           "hardware_execution_ms": hw[0], "result_accumulation_ms": ra[0], "total_ms": tot[0],
+           "calls": len(calls),
+           "median": {"hardware_execution_ms": med(hw), "result_accumulation_ms": med(ra), "total_ms": med(tot)},
+           "total_gflops_median": round(2.0 * d["nnz"] / (med(tot) * 1e-3) / 1e9, 3) if med(tot) > 0 else None,
+           "software_execution_ms": round(sw_ms, 3) if sw_ms else None,
+           "verification": [c["verification"] for c in calls],
+           "max_rel_diff_vs_spmv_gold": max(c["max_rel_diff"] for c in calls), "tol": tol,
+           "storage_mb": d["storage_mb"], "csr_mb": d["csr_mb"],
+           "child_wall_s": round(time.perf_counter() - t0, 2)}
+    res["pass"] = bool(p.returncode == 0 and all(v == 0 for v in res["verification"])
+                       and res["max_rel_diff_vs_spmv_gold"] <= tol)
+    if os.environ.get("SPMV_BENCH_INJECT") == "dropin":
+        res["verification"][0], res["pass"] = 1, False  # test hook: a failed drop-in verification
+    return res
 
 
 def lds_xtiles(lib, args, rp, col, val, x, y_ref, ncols, dev_index, stream):
@@ -680,12 +837,17 @@ def side_config(args, name, dev, stream):
     return res
 
 
-def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
+def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, y_parity=None, reps=5):
     """The y exchange through the library's own RCCL path (Part 4 of the C-ABI,
     spmv_mgpu_create_rank): rank 0's RCCL id is shared over torch.distributed, every rank joins
     with its plan, and spmv_mgpu_run times the SpMV plus each exchange form with HIP events
-    (compute / exchange, max over ranks). rank 0's gathered y is checked against a gather of the
-    same slices through torch.distributed."""
+    (compute / exchange, max over ranks).
+
+    Every form's result is verified, against this SpMV's slices all-gathered
+    through torch.distributed (independent of the library's clique) -- itself held, on rank 0, to
+    the parity gather `y_parity` that was checked against the oracle: rank 0's gathered y and
+    its reduced y (the ncclReduce of full-length partials, accum_results' += ), and every rank's
+    all-gathered next x. `verified.pass` is false on any mismatch; the caller then fails the run."""
     ok = torch.tensor([1.0], device=dev)
     uid = b"\0" * 128
     try:
@@ -714,6 +876,20 @@ def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
         return {"error": err or "spmv_mgpu_create_rank failed on another rank"}
     res = {"api": "spmv_mgpu_create_rank + spmv_mgpu_run (library RCCL clique, one rank per GPU)",
            "rccl_comm_count": mg.comm_count()}
+    # the reference y of every form: this SpMV's slices, all-gathered over torch.distributed
+    y_loc = torch.empty(int(counts[rank]), dtype=x.dtype, device=dev)
+    plan.run(x, y_loc, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    y_all = spmv_dist.exchange_allgather(y_loc, counts).to(dev).double()
+    del y_loc
+    scale = float(y_all.abs().max().clamp_min(1e-300).item())
+    tol = 1e-12 if x.element_size() == 8 else 1e-5  # two SpMVs differ in the LDS adds' order only
+    inject = os.environ.get("SPMV_BENCH_INJECT")
+
+    def rel(y_n):
+        return float((y_n.to(dev).double() - y_all).abs().max().item()) / scale
+
+    diffs = {"torch_allgather_vs_parity_gather": rel(y_parity) if (rank == 0 and y_parity is not None) else 0.0}
     mg.set_x_device(x)
     square = int(counts.sum()) == int(ncols)  # (--slice-of: the slices do not cover x; no all-gather)
     forms = [("gather", spmv_hw.MGPU_GATHER), ("reduce", spmv_hw.MGPU_REDUCE)]
@@ -732,19 +908,28 @@ def native_exchange(lib, plan, x, ncols, counts, world, rank, dev, reps=5):
             es.append(e)
         res[f"{name}_compute_ms"] = round(spmv_dist.max_over_ranks(float(np.median(cs)), dev), 5)
         res[f"{name}_exchange_ms"] = round(spmv_dist.max_over_ranks(float(np.median(es)), dev), 5)
-        if mode != spmv_hw.MGPU_ALLGATHER:  # a stream of SpMVs, each exchange under the next kernels
+        if mode == spmv_hw.MGPU_ALLGATHER:  # every rank's next x = A x
+            x_next = torch.from_numpy(mg.y(spmv_hw.MGPU_ALLGATHER))
+            if inject == "allgather" and rank == world - 1:
+                x_next[-1] += 1.0  # test hook: a wrong all-gather result on the last rank
+            diffs["allgather"] = rel(x_next)
+        else:  # a stream of SpMVs, each exchange under the next kernels; rank 0 keeps the last y
             mg.run_pipelined(mode, 2)
             res[f"{name}_pipelined_ms_per_step"] = round(
                 spmv_dist.max_over_ranks(mg.run_pipelined(mode, max(reps, 8)), dev), 5)
-        if mode == spmv_hw.MGPU_GATHER:
-            y_loc = torch.empty(int(counts[rank]), dtype=x.dtype, device=dev)
-            plan.run(x, y_loc, torch.cuda.current_stream())
-            torch.cuda.synchronize()
-            y_t = spmv_dist.exchange_gather(y_loc, counts)
+            diffs[name] = 0.0
             if rank == 0:
-                y_n = torch.from_numpy(mg.y(spmv_hw.MGPU_GATHER)).to(y_t.device)
-                res["gather_max_rel_diff_vs_torch"] = float(
-                    ((y_n.double() - y_t.double()).abs().max() / y_t.double().abs().max().clamp_min(1e-300)).item())
+                y_n = torch.from_numpy(mg.y(mode))
+                if inject == name:
+                    y_n[0] += 1.0  # test hook (tests/test_gpu_bench.py): a wrong reduce / gather result
+                diffs[name] = rel(y_n)
+    diffs = {k: spmv_dist.max_over_ranks(v, dev) for k, v in diffs.items()}
+    res["gather_max_rel_diff_vs_torch"] = diffs["gather"]
+    res["verified"] = {"against": "this SpMV's slices all-gathered over torch.distributed; on rank 0 "
+                                  "within tol of the oracle-checked parity gather",
+                       "tol": tol, "max_rel_diff": diffs,
+                       **{k: bool(v <= tol) for k, v in diffs.items()}}
+    res["verified"]["pass"] = all(v <= tol for v in diffs.values())
     # iterative use: SpMV + all-gather of y into every rank's next x, steps
     # replayed from one hipGraph per rank (spmv_mgpu_run_graph; capture outside the timing)
     if square:
@@ -845,8 +1030,7 @@ def distributed_parity(lib, args, world, rank, dev, y, st, held=None):
     regenerated on rank 0 by the same generator. Weak scaling (and the banded workload): every
     rank checks its own partition; the worst error over ranks is reported. Runs after the timed
     region, never inside it."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    oracle = _oracle()
     dtype = np.float64 if args.dtype == "f64" else np.float32
     tol = 1e-6 if dtype == np.float64 else 1e-4
 
@@ -854,6 +1038,8 @@ def distributed_parity(lib, args, world, rank, dev, y, st, held=None):
         h = [t.cpu().numpy() for t in (rp, col, val, x)]
         r, c = h[0].view(np.uint32), h[1].view(np.uint32)
         ref = oracle.spmv_gold(r, c, h[2], h[3])
+        if held is not None:
+            held["ref"] = ref  # (rank 0, strong: spmv_gold's y of the whole matrix, for the drop-in run)
         yt = y_test.cpu().numpy() if hasattr(y_test, "cpu") else y_test
         return oracle.scaled_error(r, c, h[2], h[3], ref, yt), oracle.verification_errors(ref, yt.astype(ref.dtype))
 
@@ -960,6 +1146,28 @@ def dependent_iteration(plan, x, y, st, steps, world, rank, dev, y_full, row0=0)
             "x1_max_rel_diff_vs_parity_y": diff, "tol": tol, "pass": bool(diff <= tol)}
 
 
+def value_e2e(out, ms, nnz_all):
+    """value_e2e: 2 nnz / (the serial SpMV step + the exchange that completes y), beside the
+    compute-only `value` -- the reference's "Total time" is hardware + accumulation
+    (csr_hw_wrapper.cpp:276-285). At N > 1 the exchange is the library's own RCCL reduce of
+    full-length partials (spmv_mgpu_run MGPU_REDUCE: accum_results' +=, exchange only, median
+    of 5, max over ranks, verified), else torch.distributed's reduce; at N = 1 there is none."""
+    if out["n_ranks"] == 1 and not out["dist_rehearsal"]:
+        return out["value"], {"form": "one GPU: the SpMV is the whole job (no exchange)"}
+    ex = out.get("exchange") if isinstance(out.get("exchange"), dict) else {}
+    nat = ex.get("native") if isinstance(ex.get("native"), dict) else {}
+    if "reduce_exchange_ms" in nat:
+        ex_ms, src = nat["reduce_exchange_ms"], "exchange.native.reduce_exchange_ms (library RCCL reduce)"
+    elif "reduce_ms" in ex:
+        ex_ms, src = ex["reduce_ms"], "exchange.reduce_ms (torch.distributed reduce)"
+    else:
+        return None, {"form": "no exchange was measured"}
+    return (round(2.0 * nnz_all / ((ms + ex_ms) * 1e-3) / 1e9, 3),
+            {"form": "serial SpMV step (ms_per_step) + the y reduce onto rank 0, per SpMV", "ms_per_step": ms,
+             "exchange_ms": ex_ms, "exchange_src": src,
+             "value_is": "compute-only: max-over-ranks SpMV step, no collective inside the timed step"})
+
+
 def main():
     args = parse()
     run_watchdog = arm_run_watchdog(args)
@@ -977,7 +1185,7 @@ def main():
     y = torch.empty(st["nr_rows"], dtype=x.dtype, device=dev)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
-    keep_csr = rank == 0 and not args.multi and not args.no_cpu
+    keep_csr = not args.multi  # N = 1: the full-size parity check reads the matrix after the timed region
     want_xtiles = not args.multi and args.workload == "powerlaw" and not args.no_xtiles
     if not keep_csr and not want_xtiles:
         del rp, col, val
@@ -1206,37 +1414,53 @@ def main():
             print(json.dumps(line), flush=True)
         stage("emitted" if rank == 0 else "done")
 
-    # N > 1: parity is part of the measurement, not an extra (main.cpp:77-82 verifies every
-    # spmv_hw result). It runs under the run deadline and the collective timeout only; a parity
-    # that errors or fails prints the line with it and ends the run with status 3.
+    def fail_run(what, detail):
+        """A check of what the line reports did not pass: the line is printed as an invalid
+        measurement (value null, the measured number kept as value_unverified) and the run ends
+        with status 3 on every rank -- an rc-blind reader cannot take it for a result."""
+        out.update(valid=False, error=what, value_unverified=out["value"], value=None)
+        emit()
+        print(f"bench.py rank {rank}: {what}: {detail}", file=sys.stderr, flush=True)
+        os._exit(3)
+
+    # parity is part of the measurement, not an extra (main.cpp:77-82 verifies every spmv_hw
+    # result), at every N. It runs under the run deadline and the collective timeout only, before
+    # the extras watchdog; a parity that errors or fails ends the run with status 3.
     held = {"row_begin": (desc.get("slice_rows") or [0])[0] if args.slice_of else 0}
     if os.environ.get("SPMV_BENCH_INJECT") == "parity" and rank == world - 1:
         y[0] += 1.0  # test hook (tests/test_gpu_bench.py): a wrong y must fail the run
-    if args.multi:
-        stage("parity")
-        try:
+    stage("parity")
+    hcsr = ref = sw_ms = None
+    try:
+        if args.multi:
             out["parity"] = distributed_parity(lib, args, world, rank, dev, y, st, held)
-        except Exception as e:
-            out["parity"] = {"error": f"{type(e).__name__}: {str(e)[:300]}", "pass": False}
-        if not out["parity"].get("pass"):
-            emit()
-            print(f"bench.py rank {rank}: parity did not pass: {out['parity']}", file=sys.stderr, flush=True)
-            os._exit(3)
+        else:  # N = 1: the whole matrix against spmv_gold (the CSR was kept for this)
+            hcsr = host_csr(rp, col, val, x, y)
+            del rp, col, val
+            torch.cuda.empty_cache()
+            out["parity"], ref, sw_ms = full_parity(hcsr)
+    except Exception as e:
+        out["parity"] = {"error": f"{type(e).__name__}: {str(e)[:300]}", "pass": False}
+    if not out["parity"].get("pass"):
+        fail_run("parity did not pass", out["parity"])
 
-    # what follows adds reported-only fields. Each runs under a try (reported, never fatal), and
-    # a watchdog prints the line as it stands and ends the process if they take longer than
-    # --extras-timeout seconds (a hung collective on an 8-GPU node must not cost the measured,
-    # verified value)
+    # what follows adds reported-only fields, except that every result they report is verified
+    # too (the library's RCCL forms, the drop-in's y): a mismatch fails the run (status 3). Each
+    # runs under a try (an error is reported, never fatal), and a watchdog prints the line as it
+    # stands and ends the process if they take longer than --extras-timeout seconds (a hung
+    # collective on an 8-GPU node must not cost the measured, verified value)
     stage("extras")
 
     def on_timeout():
         emit(f"extras still running after {args.extras_timeout} s; line printed without them")
         sys.stdout.flush()
+        _kill_children()
         os._exit(args.extras_timeout_status)
 
     watchdog = threading.Timer(args.extras_timeout, on_timeout)
     watchdog.daemon = True
     watchdog.start()
+    t_extras = time.monotonic()
 
     def guarded(field, fn):
         try:
@@ -1321,7 +1545,8 @@ def main():
             res["native"] = {"skipped": "ranks share one GPU; RCCL refuses two ranks on one device"}
         elif not args.no_native_exchange:
             try:
-                res["native"] = native_exchange(lib, plan, x, st["nr_cols"], counts, world, rank, dev)
+                res["native"] = native_exchange(lib, plan, x, st["nr_cols"], counts, world, rank, dev,
+                                                held.get("y_full"))
             except Exception as e:  # reported, never fatal to the bench line
                 res["native"] = {"error": str(e)[:300]}
         return res
@@ -1335,32 +1560,56 @@ def main():
             return res
         guarded("dependent", dependent)
         step_forms["dependent"] = out.pop("dependent")
-    held.clear()
     if args.multi:
         guarded("exchange", exchange_fields)
         nat = out["exchange"].get("native") if isinstance(out["exchange"], dict) else None
         if isinstance(nat, dict) and "allgather_graph_ms_per_step" in nat:
             # the same dependent form through the library's own RCCL clique, steps in one hipGraph
             step_forms["dependent_native_graph_ms_per_step"] = nat["allgather_graph_ms_per_step"]
+        if isinstance(nat, dict) and nat.get("verified", {}).get("pass") is False:  # (same on every rank)
+            fail_run("the library's RCCL exchange gave a wrong y", nat["verified"])
+    held.pop("y_full", None)
     if args.multi and args.scaling == "weak" and args.workload == "powerlaw" and not args.no_strong_companion:
         guarded("strong_companion", lambda: strong_companion(lib, args, world, rank, dev, stream))
     if args.multi and args.scaling == "strong" and args.workload == "powerlaw" and not args.no_weak_companion:
         guarded("weak_companion", lambda: weak_companion(lib, args, world, rank, dev, stream))
-    if keep_csr:
-        def cpu_fields():
-            out["cpu_baseline"], out["parity"] = cpu_baseline(lib, rp, col, val, x, y, args.cpu_reps, args.cpu_threads)
-            return out["cpu_baseline"]
-        guarded("cpu_baseline", cpu_fields)
-        del rp, col, val
-        torch.cuda.empty_cache()
+    if hcsr is not None and not args.no_cpu:
+        guarded("cpu_baseline", lambda: cpu_baseline(lib, hcsr, ref, args.cpu_reps, args.cpu_threads))
+    hcsr = None
+    # the drop-in boundary (create_csr_hw_matrix -> spmv_hw -> verification) in a child process:
+    # N = 1 one unit, host merge (the reference's CU = 1 build); N > 1 (strong, the whole matrix)
+    # rank 0 runs it with N units, one per GPU, merged by the library's RCCL reduce over xGMI --
+    # the north star's mapping of accum_results -- while the other ranks wait on the store (no
+    # GPU collective spinning on the GPUs the child uses)
+    left = args.extras_timeout - (time.monotonic() - t_extras)
+    child_timeout = max(30.0, min(240.0, left - 60.0))
+    if not args.no_dropin and not args.slice_of and (not args.multi or args.scaling == "strong"):
+        if not args.multi:
+            guarded("dropin", lambda: run_dropin(args, 1, "host", ref, sw_ms, child_timeout))
+        elif torch.cuda.device_count() < world:
+            out["dropin"] = {"skipped": f"{world} units need {world} GPUs ({torch.cuda.device_count()} here)"}
+        else:
+            res, status = spmv_dist.rank0_only(
+                lambda: run_dropin(args, world, "reduce", held["ref"], None, child_timeout), child_timeout + 60,
+                passed=lambda r: r.get("pass") is not False)
+            if rank == 0:
+                out["dropin"] = res
+            if status == "fail":
+                fail_run("the drop-in boundary's y failed verification", res or "see rank 0")
+            if status == "timeout":  # rank 0's line reports the drop-in; this rank only waited
+                print(f"bench.py rank {rank}: no drop-in status from rank 0", file=sys.stderr, flush=True)
+        if isinstance(out.get("dropin"), dict) and out["dropin"].get("pass") is False:
+            fail_run("the drop-in boundary's y failed verification", out["dropin"])
+    held.clear()
+    ref = None
     if not args.multi and args.workload == "powerlaw" and args.dtype == "f64" and not args.no_side_configs:
         guarded("side_configs", lambda: {name: side_config(args, name, dev, stream) for name in ("config2", "config5")})
+    # the end-to-end rate beside the compute-only value: one SpMV plus the
+    # exchange that completes y, as the reference's "Total time" is hardware + accumulation
+    # (csr_hw_wrapper.cpp:276-285)
+    out["value_e2e"], out["value_e2e_form"] = value_e2e(out, ms, nnz_all)
     watchdog.cancel()
     emit()
-    par = out.get("parity")
-    if isinstance(par, dict) and par.get("pass") is False:  # N = 1: the full-size check failed
-        print(f"bench.py: parity did not pass: {par}", file=sys.stderr, flush=True)
-        os._exit(3)
     # the line is out and verified: a teardown that hangs (plan or process-group destruction) must
     # not hold the run (under torch.distributed.run no parent would end it before --run-timeout)
     teardown = threading.Timer(args.spawn_grace, lambda: os._exit(0))

@@ -41,10 +41,29 @@ def parse(argv=None):
                     help="default: nccl when every rank has its own GPU, else gloo")
     ap.add_argument("--grid", type=int, default=1000)
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--tol", type=float, default=1e-8,
+                    help="exit status 2 when the final relative residual is above this")
+    ap.add_argument("--timeout", type=float, default=300.0,
+                    help="seconds the whole run may take: every collective gives up after it, and the "
+                         "parent kills ranks still running then (exit status 124)")
     return ap.parse_args(argv)
 
 
+def _die_with_parent():
+    """A rank is SIGKILLed when the parent dies (Linux prctl PR_SET_PDEATHSIG): a parent killed by
+    a test's timeout leaves no rank on the GPU."""
+    try:
+        import ctypes
+        import signal
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGKILL, 0, 0, 0)
+    except Exception:
+        pass
+
+
 def rank_main(rank, world, port, args, out_q=None):
+    _die_with_parent()
+    import datetime
+
     import torch
     import torch.distributed as dist
 
@@ -56,10 +75,12 @@ def rank_main(rank, world, port, args, out_q=None):
     ndev = torch.cuda.device_count()
     torch.cuda.set_device(rank % ndev)
     dev = torch.device("cuda", rank % ndev)
+    tmo = datetime.timedelta(seconds=args.timeout)  # every collective gives up, none waits forever
     if args.backend == "nccl":
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=tmo)
     else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=tmo)
+    res = None
     try:
         lib = spmv_hw.load(np.float64)
         rp, col, val, n = laplacian_2d(args.grid)
@@ -118,6 +139,9 @@ def rank_main(rank, world, port, args, out_q=None):
         plan.destroy()
     finally:
         dist.destroy_process_group()
+    if rank == 0 and not res <= args.tol:  # (NaN included)
+        print(f"relative residual {res:.3e} above --tol {args.tol:g}", file=sys.stderr, flush=True)
+        sys.exit(2)
 
 
 def _free_port():
@@ -134,16 +158,22 @@ def main(argv=None):
         args.backend = "nccl" if args.gpus <= torch.cuda.device_count() else "gloo"
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=rank_main, args=(r, args.gpus, port, args)) for r in range(args.gpus)]
+    procs = [ctx.Process(target=rank_main, args=(r, args.gpus, port, args), daemon=True) for r in range(args.gpus)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout=600)
+    deadline = time.monotonic() + args.timeout
+    for p in procs:  # one deadline for the whole run, not one per rank
+        p.join(timeout=max(0.0, deadline - time.monotonic()))
+    hung = [r for r, p in enumerate(procs) if p.is_alive()]
     for p in procs:
         if p.is_alive():
             p.kill()
+            p.join()
+    if hung:
+        print(f"cg_dist: ranks {hung} still running after {args.timeout:g} s, killed", file=sys.stderr, flush=True)
+        return 124
     codes = [p.exitcode for p in procs]
-    return 0 if all(c == 0 for c in codes) else 1
+    return 0 if all(c == 0 for c in codes) else max((c for c in codes if c and c > 0), default=1)
 
 
 if __name__ == "__main__":

@@ -418,23 +418,63 @@ static int build_layout(spmv_plan &P, int kernel, bool automatic, const IndexTyp
     return 0;
 }
 
-// Mean time of 3 SpMVs (after one warm-up) with scratch x/y, for SPMV_HW_KERNEL=tune.
+// ms per SpMV of a layout with scratch x/y, for SPMV_HW_KERNEL=tune: kTuneSteps serial SpMVs
+// captured into one hipGraph on a private stream (no host launch gap inside a sample), replayed
+// once to warm, then kTuneReps replays each timed with its own event pair; the median replay / steps.
+// One timed launch per candidate (round 4) let the timer's noise pick the layout.
+constexpr int kTuneSteps = 4, kTuneReps = 7;
 static int time_layout(spmv_plan &P, const ValueType *d_x, ValueType *d_y, hipStream_t s, double *ms)
 {
-    hipEvent_t e0, e1;
-    SPMV_TRY(hipEventCreate(&e0));
-    SPMV_TRY(hipEventCreate(&e1));
-    int rc = ::run_impl(&P, d_x, d_y, s, false);
-    (void)hipEventRecord(e0, s);
-    for (int i = 0; i < 3 && !rc; ++i)
-        rc = ::run_impl(&P, d_x, d_y, s, false);
-    (void)hipEventRecord(e1, s);
-    float t = 0.f;
-    if (!rc && hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess)
-        *ms = t / 3.0;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    return rc;
+    SPMV_TRY(hipStreamSynchronize(s));  // the layout was built on s
+    struct Res {
+        hipStream_t ts = nullptr;
+        hipGraphExec_t ge = nullptr;
+        hipEvent_t ev[2 * kTuneReps] = {};
+        ~Res()
+        {
+            for (hipEvent_t e : ev)
+                if (e)
+                    (void)hipEventDestroy(e);
+            if (ge)
+                (void)hipGraphExecDestroy(ge);
+            if (ts)
+                (void)hipStreamDestroy(ts);
+        }
+    } r;
+    SPMV_TRY(hipStreamCreateWithFlags(&r.ts, hipStreamNonBlocking));
+    for (hipEvent_t &e : r.ev)
+        SPMV_TRY(hipEventCreate(&e));
+    SPMV_TRY(hipStreamBeginCapture(r.ts, hipStreamCaptureModeRelaxed));
+    int rc = 0;
+    for (int i = 0; i < kTuneSteps && !rc; ++i)
+        rc = ::run_impl(&P, d_x, d_y, r.ts, false);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(r.ts, &g);
+    if (rc) {
+        if (g)
+            (void)hipGraphDestroy(g);
+        return rc;
+    }
+    SPMV_TRY(ec);
+    const hipError_t ei = hipGraphInstantiate(&r.ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    SPMV_TRY(ei);
+    SPMV_TRY(hipGraphLaunch(r.ge, r.ts));  // warm
+    for (int k = 0; k < kTuneReps; ++k) {
+        SPMV_TRY(hipEventRecord(r.ev[2 * k], r.ts));
+        SPMV_TRY(hipGraphLaunch(r.ge, r.ts));
+        SPMV_TRY(hipEventRecord(r.ev[2 * k + 1], r.ts));
+    }
+    SPMV_TRY(hipStreamSynchronize(r.ts));
+    std::vector<double> t(kTuneReps);
+    for (int k = 0; k < kTuneReps; ++k) {
+        float v = 0.f;
+        SPMV_TRY(hipEventElapsedTime(&v, r.ev[2 * k], r.ev[2 * k + 1]));
+        t[k] = v / kTuneSteps;
+    }
+    std::nth_element(t.begin(), t.begin() + kTuneReps / 2, t.end());
+    *ms = t[kTuneReps / 2];
+    return 0;
 }
 
 int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows, IndexType nr_cols,
@@ -501,7 +541,8 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
     }
 
     int kernel = requested_kernel();
-    if (kernel == -1) {
+    const bool tune = kernel == kKernelTune;
+    if (kernel == -1 || tune) {  // (tune: the automatic choice is the preferred candidate)
         // automatic choice: the sweep pays once x outgrows ~half an XCD's L2 and the columns of a
         // row are scattered: fewer than 30 % of the consecutive column pairs of sampled rows lie
         // < 64 apart (random: ~0; 2-D 5-point stencil 0.5, 3-D 7-point 0.33, 27-point 0.69, where
@@ -533,6 +574,9 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
             !(det && det[0] == '1'))
             kernel = kKernelBinned;
     }
+    const int auto_kernel = kernel;
+    if (tune)
+        kernel = kKernelTune;
     trace("validate + kernel choice", s);
     if (const char *t = ablation_env("SPMV_SWEEP_THREADS")) {
         const int v = std::atoi(t);
@@ -552,41 +596,58 @@ int plan_create_from_host_rowptr(spmv_plan **out, int device, IndexType nr_rows,
         return q;
     };
     if (kernel == kKernelTune) {
-        // build the tile, sweep, slice and binned layouts one at a time, time one SpMV of each on
-        // this matrix, keep the fastest: only the best so far and the candidate are resident, and
-        // a candidate whose build fails (e.g. out of memory) is dropped, not a plan error. The
-        // tiles are the fallback every matrix builds. With SPMV_SWEEP_DETERMINISTIC=1 the binned
-        // layout (pass-2 adds in timing order) is not a candidate: the switch promises fixed bits.
+        // build the tile, sweep, slice and binned layouts one at a time and time each on this
+        // matrix (time_layout: median of graph-replayed samples). The candidates go in preference
+        // order -- the automatic choice first, then tiles, sweep, slices, binned -- and a later one
+        // replaces the kept layout only when it is more than 3 % faster, so two layouts within
+        // the timer's noise of each other cannot trade places between two builds of one matrix.
+        // Only the kept layout and the candidate are resident; a candidate whose build fails
+        // (e.g. out of memory) is dropped, not a plan error. With SPMV_SWEEP_DETERMINISTIC=1 the
+        // binned layout (pass-2 adds in timing order) is not a candidate: the switch promises
+        // fixed bits.
         const char *det = std::getenv("SPMV_SWEEP_DETERMINISTIC");
         const bool fixed_bits = det && det[0] == '1';
+        constexpr double kTuneBand = 0.97;
         Tmp tx, ty;
         SPMV_TRY(hipMalloc(&tx.p, std::max<size_t>(nr_cols, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMalloc(&ty.p, std::max<size_t>(nr_rows, 1) * sizeof(ValueType)));
         SPMV_TRY(hipMemsetAsync(tx.p, 0, std::max<size_t>(nr_cols, 1) * sizeof(ValueType), s));
+        const int slot_of[7] = {0, -1, 1, -1, -1, 2, 3};  // kernel id -> tuned_ms slot
+        std::vector<int> order = {auto_kernel};
+        for (int k : {kKernelTiles, kKernelSweep, kKernelSlices, kKernelBinned})
+            if (k != auto_kernel)
+                order.push_back(k);
         double tuned[4] = {1e30, 1e30, 1e30, 1e30};
-        if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s) ||
-            time_layout(*p, (const ValueType *)tx.p, (ValueType *)ty.p, s, &tuned[0]))
-            return 1;
-        double best = tuned[0];
-        const int cand[3] = {kKernelSweep, kKernelSlices, kKernelBinned};
-        for (int c = 0; c < 3; ++c) {
-            if (cand[c] == kKernelBinned && fixed_bits)
+        std::unique_ptr<spmv_plan> kept;
+        double kept_ms = 1e30;
+        for (int k : order) {
+            if (k == kKernelBinned && fixed_bits)
                 continue;
             std::unique_ptr<spmv_plan> q = fresh();
-            if (cand[c] == kKernelSlices)
+            if (k == kKernelSlices)
                 q->slice_pad_limit = 2.0;  // a slice layout padded beyond 2x is built as tiles instead
-            if (build_layout(*q, cand[c], true, h_row_ptr, d_col, d_val, s) ||
-                time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &tuned[c + 1])) {
-                tuned[c + 1] = 1e30;  // not a candidate
-                q.reset();
+            double t = 1e30;
+            if (build_layout(*q, k, true, h_row_ptr, d_col, d_val, s) ||
+                time_layout(*q, (const ValueType *)tx.p, (ValueType *)ty.p, s, &t)) {
+                q.reset();  // not a candidate
                 (void)hipGetLastError();
                 continue;
             }
-            if (tuned[c + 1] < best) {  // ties keep the earlier layout (the tiles first)
-                best = tuned[c + 1];
-                p.swap(q);
+            tuned[slot_of[k]] = t;
+            if (!kept || t < kTuneBand * kept_ms) {
+                kept.swap(q);
+                kept_ms = t;
             }
         }
+        if (!kept) {  // every candidate failed: the tiles, untimed (their error is the plan's)
+            if (build_layout(*p, kKernelTiles, true, h_row_ptr, d_col, d_val, s))
+                return 1;
+        } else {
+            p.swap(kept);
+        }
+        if (std::getenv("SPMV_HW_TRACE"))
+            std::fprintf(stderr, "spmv_hw trace: tune ms tiles %.4f sweep %.4f slices %.4f binned %.4f -> kernel %d\n",
+                         tuned[0], tuned[1], tuned[2], tuned[3], p->kernel);
         for (int c = 0; c < 4; ++c)
             p->tuned_ms[c] = tuned[c];
         trace("tune: build + time each", s);
@@ -1064,9 +1125,11 @@ int spmv_plan_set_variant(spmv_plan *p, int variant)
         set_error("spmv_plan_set_variant: measurement variant (tools library only)");
         return 1;
     }
+#endif
+    // 0 = the plan's default form in both builds: for a sweep plan that is 28 (the tools
+    // library's unpacked measurement form that used to sit at 0 is variant 40)
     if (p->kernel == kKernelSweep && variant == 0)
         variant = 28;
-#endif
     if (p->kernel == kKernelSweep) {
         // every variant but the default (28), 36 (the same) and the measurement build's stealing
         // variants 37-39 reads the 12-byte rc words, which a delta plan rebuilds on first use

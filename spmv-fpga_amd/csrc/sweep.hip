@@ -1260,7 +1260,7 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     }
     switch (p.sweep_variant) {
 #ifdef SPMV_ABLATIONS
-    case 0: SWEEP(4, 1, false, false); break;  // measurement variants of the unpacked form
+    case 40: SWEEP(4, 1, false, false); break;  // measurement variants of the unpacked form
     case 1: SWEEP(4, 1, false, true); break;
     case 3: SWEEP(4, 1, true, true); break;
     case 7: SWEEP(4, 2, true, true); break;

@@ -185,6 +185,35 @@ def sum_over_ranks(values, device):
     return [float(v) for v in t.tolist()]
 
 
+_RANK0_CALLS = [0]
+
+
+def rank0_only(fn, timeout_s: float, passed=lambda r: True):
+    """fn() on rank 0 while every other rank waits on the process group's store -- host only, so
+    no collective kernel spins on the GPUs fn may drive itself (bench.py's N-unit drop-in child
+    uses every GPU of the node). Returns (fn's result on rank 0, None elsewhere; status), status
+    the same on every rank that saw it: "ok", "fail" (passed(result) is false), "error" (fn
+    raised on rank 0; the result is then {"error": ...}) or, on a waiting rank, "timeout" when
+    rank 0 gave no status within timeout_s."""
+    import datetime
+    _RANK0_CALLS[0] += 1
+    key = f"spmv_rank0_only_{_RANK0_CALLS[0]}"
+    store = dist.distributed_c10d._get_default_store()
+    if dist.get_rank() == 0:
+        try:
+            res = fn()
+            status = "ok" if passed(res) else "fail"
+        except Exception as e:
+            res, status = {"error": f"{type(e).__name__}: {str(e)[:300]}"}, "error"
+        store.set(key, status)
+        return res, status
+    try:
+        store.wait([key], datetime.timedelta(seconds=timeout_s))
+        return None, store.get(key).decode()
+    except Exception:
+        return None, "timeout"
+
+
 def slice_counts(bounds) -> np.ndarray:
     b = np.asarray(bounds, np.int64)
     return np.diff(b)

@@ -140,3 +140,34 @@ def test_slice_of_needs_the_rehearsal_and_the_strong_cut():
     assert p.returncode == 2 and "strong-scaling cut" in p.stderr
     p = _run("--dist-rehearsal", "--slice-of", "8", "--dry-launch")
     assert p.returncode == 0, p.stderr
+
+
+@pytest.mark.parametrize("extra,multi", [((), False), (("--gpus", "8"), True), (("--dist-rehearsal",), True)])
+def test_default_deadlines_fit_the_driver_limit(extra, multi):
+    """the run's own deadline (and the self-launch parent's kill after it) ends
+    before the driver's 600 s limit, so a hung run still prints its stage line; a collective gives
+    up long before the run deadline; the extras watchdog fires before it even when the extras
+    start late (N = 1 by half the deadline, N > 1 by 5/8 of it)."""
+    p = _run(*extra, "--dry-launch")
+    assert p.returncode == 0, p.stderr
+    d = _lines(p.stdout)[0]["deadlines"]
+    limit = _lines(p.stdout)[0]["driver_limit_s"]
+    assert limit == 600
+    assert d["run_timeout"] <= 480 and d["run_timeout"] + d["spawn_grace"] < limit
+    assert d["collective_timeout"] <= d["run_timeout"] / 4
+    frac = 0.625 if multi else 0.5
+    assert d["extras_timeout"] + frac * d["run_timeout"] <= d["run_timeout"]
+    # explicit deadlines derive the others
+    p = _run(*extra, "--dry-launch", "--run-timeout", "200")
+    d = _lines(p.stdout)[0]["deadlines"]
+    assert d["run_timeout"] == 200 and d["collective_timeout"] == 50 and d["extras_timeout"] == (75 if multi else 100)
+
+
+def test_self_launch_rank0_alone_after_the_others_finished_is_not_hung():
+    """ranks 1 and 2 finished cleanly ("done", status 0) while rank 0 still works after
+    the last collective (the drop-in child, the CPU baseline): it is not killed at --spawn-grace,
+    only the run deadline bounds it (here: killed at --run-timeout, status 124)."""
+    p = _run("--gpus", "3", "--dry-launch", "--dry-launch-rc", "0:hang", "--spawn-grace", "1", "--run-timeout", "6",
+             timeout=60)
+    assert p.returncode == 124, (p.returncode, p.stderr)
+    assert "run timeout" in p.stderr

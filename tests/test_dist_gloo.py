@@ -115,3 +115,59 @@ def test_row_sliced_exchange_rebuilds_y(world, mode):
     assert ok, "exchanged y differs from the single-process oracle"
     assert m == world - 1
     assert sum(counts) == 20_000 and min(counts) > 0
+
+
+def _rank0_worker(rank, world, port, q):
+    for p in (ROOT, os.path.join(ROOT, "spmv-fpga_amd")):
+        sys.path.insert(0, p)
+    import time
+
+    import torch.distributed as dist
+
+    import spmv_dist as sdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        got = []
+
+        def work(result):
+            def fn():
+                time.sleep(0.5)  # the waiting ranks block on the store meanwhile
+                if result is None:
+                    raise RuntimeError("boom")
+                return result
+            return fn
+
+        for result in ({"pass": True}, {"pass": False}, None):
+            got.append(sdist.rank0_only(work(result), 30, passed=lambda r: r.get("pass") is not False))
+        # rank 0 never answers a fourth call: the other ranks give up after their timeout
+        if rank == 0:
+            got.append((None, "skipped"))
+        else:
+            got.append(sdist.rank0_only(lambda: None, 1))
+        dist.barrier()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank0_only_waits_on_the_store(world):
+    """bench.py's N-unit drop-in run at N > 1: rank 0 alone runs the child (every GPU of the node)
+    while the other ranks wait on the process group's store, not in a GPU collective; every rank
+    learns whether rank 0's result passed, and a waiting rank gives up after its timeout."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank0_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert [s for _, s in res[0]] == ["ok", "fail", "error", "skipped"]
+    assert res[0][0][0] == {"pass": True} and "boom" in res[0][2][0]["error"]
+    for r in range(1, world):
+        assert res[r] == [(None, "ok"), (None, "fail"), (None, "error"), (None, "timeout")]

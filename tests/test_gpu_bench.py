@@ -52,6 +52,16 @@ def test_bench_one_gpu_line():
     sf = d["step_forms"]  # value is the serial chain (each SpMV complete before the next)
     assert sf["value_form"] == "serial" and sf["serial_ms_per_step"] == d["ms_per_step"]
     assert d["graph"]["run_graph_ms_per_step"] > 0
+    assert d["value_e2e"] == d["value"]  # one GPU: no exchange
+    # the drop-in boundary: the reference's run.elf figures, verified
+    di = d["dropin"]
+    assert di["pass"] and di["units"] == 1 and di["merge"] == "host", di
+    assert di["calls"] == 5 and di["verification"] == [0] * 5 and di["max_rel_diff_vs_spmv_gold"] <= 1e-12
+    assert di["rows"] == 400_000 and di["nnz"] == 6_400_000
+    for k in ("matrix_read_ms", "hardware_execution_ms", "result_accumulation_ms", "total_ms"):
+        assert di[k] > 0, (k, di)
+    assert abs(di["total_ms"] - di["hardware_execution_ms"] - di["result_accumulation_ms"]) < 1e-3
+    assert di["software_execution_ms"] > 0 and di["storage_mb"] > 0
 
 
 @pytest.mark.parametrize("scaling", ["strong", "weak"])
@@ -93,6 +103,14 @@ def test_bench_one_rank_rccl_rehearsal(scaling):
         nat = ex["native"]
         assert "error" not in nat, nat
         assert nat["rccl_comm_count"] == 1 and nat["gather_max_rel_diff_vs_torch"] <= 1e-12  # two SpMVs (LDS adds)
+        v = nat["verified"]  # every form of the library's exchange is checked
+        assert v["pass"] and v["gather"] and v["reduce"] and v["allgather"], v
+        assert v["max_rel_diff"]["torch_allgather_vs_parity_gather"] <= 1e-12
+        # the north star's literal mapping at world 1: spmv_hw with one unit, RCCL reduce merge
+        di = d["dropin"]
+        assert di["pass"] and di["units"] == 1 and di["merge"] == "reduce", di
+        e2e = d["value_e2e_form"]
+        assert d["value_e2e"] < d["value"] and e2e["exchange_ms"] == nat["reduce_exchange_ms"], e2e
         assert all(nat[k] > 0 for k in ("gather_compute_ms", "reduce_exchange_ms", "allgather_graph_ms_per_step"))
         sf = d["step_forms"]
         assert sf["dependent"]["pass"] and sf["dependent_ms_per_step"] > 0
@@ -134,3 +152,41 @@ def test_bench_hung_rank_ends_at_the_run_timeout():
     (line,) = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert line["value"] is None and "run timeout" in line["error"]
     assert line["stage"] == {"0": "timed", "1": "timed"}, line
+
+
+def test_bench_one_gpu_parity_failure_fails_the_run():
+    """at N = 1 the full-size parity check is part of the measurement. A wrong
+    y (SPMV_BENCH_INJECT=parity) gives an invalid line -- value null, the measured number kept as
+    value_unverified -- and exit status 3, before any extra runs."""
+    d = _bench("--no-side-configs", "--no-xtiles", "--no-det", "--cpu-reps", "1",
+               env={"SPMV_BENCH_INJECT": "parity"}, want_rc=3)
+    assert d["parity"]["pass"] is False and d["value"] is None and d["valid"] is False
+    assert d["value_unverified"] > 0 and d["cpu_baseline"] is None and "dropin" not in d
+
+
+def test_bench_one_gpu_extras_timeout_keeps_the_verified_parity():
+    """An N = 1 run whose extras outlast --extras-timeout prints the line from the watchdog (exit
+    --extras-timeout-status, 0 by default) and still carries the passed full-size parity."""
+    d = _bench("--no-xtiles", "--no-det", "--extras-timeout", "0.5", "--cpu-reps", "50")
+    assert d["extras_timeout"] and d["parity"]["pass"] and d["value"] > 0
+    assert d["parity"]["rows_checked"] == 400_000
+
+
+def test_bench_failed_dropin_verification_fails_the_run():
+    """A drop-in call whose verification is not 0 (test hook SPMV_BENCH_INJECT=dropin) is a
+    result the line would report wrong: status 3, value null."""
+    d = _bench("--no-side-configs", "--no-xtiles", "--no-det", "--cpu-reps", "1", "--dropin-reps", "1",
+               env={"SPMV_BENCH_INJECT": "dropin"}, want_rc=3)
+    assert d["dropin"]["pass"] is False and d["value"] is None and d["parity"]["pass"]
+
+
+@pytest.mark.parametrize("form", ["reduce", "allgather"])
+def test_bench_wrong_library_exchange_fails_the_run(form):
+    """the library's RCCL reduce (rank 0's y) and all-gather (every rank's
+    next x) are verified, not only timed. A wrong result (SPMV_BENCH_INJECT=reduce / allgather)
+    fails the run with status 3 and names the form."""
+    d = _bench("--dist-rehearsal", "--scaling", "strong", "--no-weak-companion", "--no-dropin",
+               env={"SPMV_BENCH_INJECT": form}, want_rc=3)
+    v = d["exchange"]["native"]["verified"]
+    assert v["pass"] is False and v[form] is False and d["value"] is None, v
+    assert all(v[k] for k in ("gather", "reduce", "allgather") if k != form)

@@ -28,7 +28,7 @@ def test_distributed_cg_example_converges(gpus, backend):
     all-reduces and p all-gathered every iteration (the dependent form); two gloo ranks share
     the box's GPU, and one RCCL rank runs the nccl path. Converges like the one-GPU example."""
     cmd = [sys.executable, os.path.join(ROOT, "examples", "cg_dist.py"), "--gpus", str(gpus), "--backend", backend,
-           "--grid", "300", "--iters", "150"]
+           "--grid", "300", "--iters", "150", "--timeout", "90"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stdout + out.stderr
     res = float(out.stdout.split("relative residual")[1].split()[0])

@@ -40,7 +40,7 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py ;;
     bench32) run bench_f32 600 python bench.py --dtype f32 --no-cpu ;;
     banded) run bench_banded 300 python bench.py --workload banded ;;
-    prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --no-dropin --steps 20 ;;
     calib) [ -x tools/hbm_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/hbm_calib.hip -o tools/hbm_calib
            run calib 300 tools/hbm_calib ;;
     strong) run strong 600 python tools/strong_slices.py ${STRONG_ARGS:-} ;;
@@ -66,15 +66,15 @@ for s in $STEPS; do
            run pmc_$tagc 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$tagc" -o run -- python tools/ab_variants.py --workload powerlaw --variants sweep:3,sweep:11 --rounds 1 --reps 3
          done ;;
     pmcw) for wl in powerlaw banded; do for dt in f64 f32; do for c in FETCH_SIZE WRITE_SIZE TCC_HIT_sum TCC_MISS_sum; do
-           run pmc_${wl}_${dt}_$c 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_${dt}_$c" -o run -- python bench.py --workload $wl --dtype $dt --no-cpu --no-xtiles --no-side-configs --steps 5 --warmup 1
+           run pmc_${wl}_${dt}_$c 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_${dt}_$c" -o run -- python bench.py --workload $wl --dtype $dt --no-cpu --no-dropin --no-xtiles --no-side-configs --steps 5 --warmup 1
          done; done; done
          python tools/pmc_traffic.py "$OUT" --out "$OUT/traffic.json" > /dev/null ;;
     pmcw64) for wl in powerlaw banded; do for c in FETCH_SIZE WRITE_SIZE TCC_HIT_sum TCC_MISS_sum; do
-           run pmc_${wl}_f64_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_f64_$c" -o run -- python bench.py --workload $wl --dtype f64 --no-cpu --no-xtiles --no-side-configs --no-det --steps 5 --warmup 1
+           run pmc_${wl}_f64_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_f64_$c" -o run -- python bench.py --workload $wl --dtype f64 --no-cpu --no-dropin --no-xtiles --no-side-configs --no-det --steps 5 --warmup 1
          done; done
          python tools/pmc_traffic.py "$OUT" --out "$OUT/traffic.json" > /dev/null ;;
     pmcbin) for c in FETCH_SIZE WRITE_SIZE; do
-           run pmcbin_f32_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmcbin_f32_$c" -o run -- python bench.py --dtype f32 --no-cpu --no-xtiles --no-side-configs --no-det --steps 5 --warmup 1
+           run pmcbin_f32_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmcbin_f32_$c" -o run -- python bench.py --dtype f32 --no-cpu --no-dropin --no-xtiles --no-side-configs --no-det --steps 5 --warmup 1
          done
          python tools/pmc_binned.py "$OUT" --out "$OUT/binned_pmc.json" --session "$(basename $OUT)" ;;
     pmcx) i=0; for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM" \
