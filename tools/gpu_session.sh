@@ -15,10 +15,12 @@ run() {  # name seconds cmd...
   echo "== $name: $*" | tee -a "$OUT/session.log"
   # heartbeat: a step that prints nothing for minutes (a bench before its one line) still shows life
   ( while sleep 30; do date +%T >> "$OUT/heartbeat"; done ) & local hb=$!
+  local t0=$(date +%s%N)
   timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
+  local wall=$(( ($(date +%s%N) - t0) / 1000000 ))
   kill $hb 2>/dev/null; wait $hb 2>/dev/null
-  echo "== $name rc=$rc" | tee -a "$OUT/session.log"
+  echo "== $name rc=$rc wall_ms=$wall" | tee -a "$OUT/session.log"
   tail -5 "$OUT/$name.log"
   if fatal $rc; then echo "FATAL step $name rc=$rc; stopping" | tee -a "$OUT/session.log"; exit $rc; fi
   return 0
