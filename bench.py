@@ -605,6 +605,8 @@ def run_dropin(args, units, merge, ref, sw_ms, timeout):
            "hardware_execution_ms": hw[0], "result_accumulation_ms": ra[0], "total_ms": tot[0],
            "calls": len(calls),
            "median": {"hardware_execution_ms": med(hw), "result_accumulation_ms": med(ra), "total_ms": med(tot)},
+           "per_call_ms": {"hardware_execution": hw, "result_accumulation": ra, "total": tot,
+                           "spmv_hw_wall": [c["wall_ms"] for c in calls]},
            "total_gflops_median": round(2.0 * d["nnz"] / (med(tot) * 1e-3) / 1e9, 3) if med(tot) > 0 else None,
            "software_execution_ms": round(sw_ms, 3) if sw_ms else None,
            "verification": [c["verification"] for c in calls],
