@@ -19,6 +19,7 @@
 #include <iostream>
 #include <atomic>
 #include <mutex>
+#include <functional>
 #include <thread>
 
 #include "spmv_internal.hpp"
@@ -105,6 +106,14 @@ struct hw_matrix_impl {
     ValueType *d_y = nullptr;
     ValueType *h_stage = nullptr;
     d2h_events done;  // of the y copy's pieces
+    // streamed copy-back (plans whose sweep flags each panel's y, sweep_can_flag_panels): the
+    // panel flags in pinned host memory, the call's epoch, the panels' row bounds and the stream
+    // the pieces' copies run on while the kernel still sweeps
+    uint32_t *h_flags = nullptr;
+    uint32_t *d_flags = nullptr;
+    uint32_t epoch = 0;
+    std::vector<uint32_t> panel_rows;
+    hipStream_t copy_stream = nullptr;
     BusDataType *sub[1] = {nullptr};
     IndexType nr_rows[1] = {0}, nr_cols[1] = {0}, nr_nzeros[1] = {0}, nr_ci[1] = {0}, nr_val[1] = {0};
 };
@@ -177,6 +186,36 @@ int merge_mode(int units)
     return m;
 }
 
+// spmv_hw copies a unit's y back while its sweep still runs (SPMV_HW_STREAM, default on; 0 off)
+bool stream_enabled()
+{
+    const char *e = std::getenv("SPMV_HW_STREAM");
+    return !(e && e[0] == '0');
+}
+
+// streamed copy-back of unit m (host merge): pinned panel flags the sweep kernel writes, the
+// panels' row bounds on the host and a copy stream (its first large copy run here, like the
+// unit stream's)
+void setup_streaming(hw_matrix_impl *m)
+{
+    const spmv_plan &pl = *m->plan;
+    if (!sweep_can_flag_panels(pl) || m->row_end == m->row_begin)
+        return;
+    check(hipSetDevice(m->device), "hipSetDevice");
+    m->panel_rows.resize(pl.npanels + 1);
+    check(hipMemcpy(m->panel_rows.data(), pl.d_panel_row, (pl.npanels + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost),
+          "panel rows");
+    check(hipHostMalloc((void **)&m->h_flags, pl.npanels * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped),
+          "hipHostMalloc(panel flags)");
+    std::memset(m->h_flags, 0, pl.npanels * sizeof(uint32_t));
+    check(hipHostGetDevicePointer((void **)&m->d_flags, m->h_flags, 0), "hipHostGetDevicePointer(panel flags)");
+    check(hipStreamCreateWithFlags(&m->copy_stream, hipStreamNonBlocking), "hipStreamCreate");
+    const uint64_t rows = m->row_end - m->row_begin;
+    check(hipMemcpyAsync(m->h_stage, m->d_y, rows * sizeof(ValueType), hipMemcpyDeviceToHost, m->copy_stream),
+          "warm D2H");
+    check(hipStreamSynchronize(m->copy_stream), "warm D2H");
+}
+
 int env_pieces(int dflt)
 {
     const char *e = ablation_env("SPMV_HW_PIECES");
@@ -218,11 +257,82 @@ int wait_event(void *ready, std::string *err)
     return e != hipSuccess;
 }
 
+// One piece of a streamed copy-back: rows [b, e) of unit m's slice = its panels [q0, q1). The
+// feeder thread records `ev` after the piece's copy once every panel of it is flagged; until
+// then an adding thread waits on `state` (0 pending, 1 copy enqueued, -1 failed).
+struct streamed_piece {
+    hw_matrix_impl *m = nullptr;
+    uint32_t q0 = 0, q1 = 0;
+    uint64_t b = 0, e = 0;
+    hipEvent_t ev = nullptr;
+    std::atomic<int> state{0};
+    std::string err;
+};
+
+int wait_streamed(void *ready, std::string *err)
+{
+    auto *pc = static_cast<streamed_piece *>(ready);
+    int st;
+    while ((st = pc->state.load(std::memory_order_acquire)) == 0)
+        std::this_thread::yield();
+    if (st < 0) {
+        *err = pc->err;
+        return 1;
+    }
+    return wait_event(pc->ev, err);
+}
+
+// Copy each piece as soon as its panels are flagged, in landing order. A piece whose flags do
+// not all arrive is copied once its unit's kernels have ended (y is final then), so the feeder
+// ends whatever the kernel did; a failed kernel or copy marks the rest of the pieces failed.
+void feed_pieces(std::vector<streamed_piece> &pcs)
+{
+    std::string fail;
+    for (streamed_piece &pc : pcs) {
+        hw_matrix_impl *m = pc.m;
+        if (fail.empty()) {
+            for (uint32_t spin = 0;; ++spin) {
+                bool all = true;
+                for (uint32_t q = pc.q0; q < pc.q1 && all; ++q)
+                    all = __atomic_load_n(&m->h_flags[q], __ATOMIC_ACQUIRE) == m->epoch;
+                if (all)
+                    break;
+                if (spin % 64 == 63) {  // every ~64 polls: has the unit's launch ended anyway?
+                    const hipError_t q = hipStreamQuery(unit_stream(m->unit));
+                    if (q == hipSuccess)
+                        break;
+                    if (q != hipErrorNotReady) {
+                        fail = std::string("spmv kernels: ") + hipGetErrorString(q);
+                        break;
+                    }
+                }
+                std::this_thread::yield();
+            }
+        }
+        if (fail.empty()) {
+            hipError_t e = hipSetDevice(m->device);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(m->h_stage + pc.b, m->d_y + pc.b, (pc.e - pc.b) * sizeof(ValueType),
+                                   hipMemcpyDeviceToHost, m->copy_stream);
+            if (e == hipSuccess)
+                e = hipEventRecord(pc.ev, m->copy_stream);
+            if (e != hipSuccess)
+                fail = std::string("y copy: ") + hipGetErrorString(e);
+        }
+        if (!fail.empty()) {
+            pc.err = fail;
+            pc.state.store(-1, std::memory_order_release);
+        } else {
+            pc.state.store(1, std::memory_order_release);
+        }
+    }
+}
+
 // accum_results' '+=' of the landed pieces into the caller's y (spmv_host.hpp, host.cpp) on up
 // to 16 host threads; returns when (timestamp_us) the last copy was seen complete. The
 // documented knob SPMV_HW_PREFAULT=0 lets the adds take the page faults; the split and thread
 // count are switches of the tools build.
-double accumulate(const std::vector<add_part> &parts)
+double accumulate(const std::vector<add_part> &parts, int (*wait)(void *, std::string *) = wait_event)
 {
     accum_options o;
     const char *pf = std::getenv("SPMV_HW_PREFAULT");
@@ -233,10 +343,97 @@ double accumulate(const std::vector<add_part> &parts)
         o.threads = std::max(1, std::atoi(te));
     bool failed = false;
     std::string err;
-    const double landed = host_accumulate(parts.data(), parts.size(), wait_event, o, &failed, &err);
+    const double landed = host_accumulate(parts.data(), parts.size(), wait, o, &failed, &err);
     if (failed)
         die(err);
     return landed;
+}
+
+// spmv_hw with the host merge on plans whose sweep flags each panel (csr_hw_wrapper.cpp:193-288):
+// every unit's kernel is launched with this call's epoch; a feeder thread copies each piece of
+// y (8 pieces in all, whole panels each) as soon as its panels are flagged, and the adding
+// threads add every piece as soon as it landed -- so the PCIe copy-back and the host '+=' run
+// while the SpMV still sweeps, instead of after it. The printed times keep the reference's
+// meaning: "Hardware execution" ends when every unit's kernels have ended, "Result accumulation"
+// when the last add is done (what of it was overlapped is no longer counted there).
+void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, csr_vector *y_fpga, bool trace)
+{
+    auto tr = [&](const char *what, double since) {
+        if (trace)
+            std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", what, (timestamp_us() - since) / 1000);
+    };
+    // pieces: piece j of every unit, then j + 1 (landing order); each piece whole panels
+    std::vector<std::pair<hw_matrix_impl *, uint32_t>> cuts;  // (unit, pieces)
+    size_t n = 0;
+    for (int u = 0; u < units; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        if (m->row_end == m->row_begin)
+            continue;
+        const uint64_t rows = m->row_end - m->row_begin;
+        const uint32_t P = (uint32_t)m->panel_rows.size() - 1;
+        const uint32_t k = std::min<uint32_t>(P, rows < (1u << 18) ? 1u : (uint32_t)std::max(2, env_pieces(8) / units));
+        cuts.push_back({m, k});
+        n += k;
+    }
+    std::vector<streamed_piece> pcs(n);
+    size_t i = 0;
+    for (uint32_t j = 0, more = 1; more; ++j) {
+        more = 0;
+        for (auto &c : cuts) {
+            if (j >= c.second)
+                continue;
+            more = 1;
+            hw_matrix_impl *m = c.first;
+            const uint32_t P = (uint32_t)m->panel_rows.size() - 1;
+            streamed_piece &pc = pcs[i++];
+            pc.m = m;
+            pc.q0 = (uint32_t)(uint64_t(P) * j / c.second);
+            pc.q1 = (uint32_t)(uint64_t(P) * (j + 1) / c.second);
+            pc.b = m->panel_rows[pc.q0];
+            pc.e = m->panel_rows[pc.q1];
+            m->done.device = m->device;
+            pc.ev = m->done.get(j);
+        }
+    }
+    std::vector<add_part> parts(n);
+    for (size_t k = 0; k < n; ++k)
+        parts[k] = {y_fpga->values + pcs[k].m->row_begin + pcs[k].b, pcs[k].m->h_stage + pcs[k].b, pcs[k].e - pcs[k].b,
+                    static_cast<void *>(&pcs[k])};
+
+    const double hw_s = timestamp_us();
+    for (int u = 0; u < units; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        if (m->row_end == m->row_begin)
+            continue;
+        if (++m->epoch == 0)  // (0 is the flags' initial value)
+            m->epoch = 1;
+        m->plan->y_flag = m->d_flags;
+        m->plan->y_epoch = m->epoch;
+        const int rc = spmv_plan_run(m->plan, x->per_device[m->device], m->d_y, unit_stream(u));
+        m->plan->y_flag = nullptr;
+        if (rc)
+            die(std::string("spmv_hw: ") + spmv_hw_last_error());
+    }
+    tr("spmv_hw: launches", hw_s);
+    std::thread feeder(feed_pieces, std::ref(pcs));
+    double landed = 0.0;
+    std::thread adder([&] { landed = accumulate(parts, wait_streamed); });
+    for (int u = 0; u < units; ++u) {
+        check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
+        check(hipStreamSynchronize(unit_stream(u)), "spmv kernels");
+    }
+    const double hw_f = timestamp_us();
+    const double hw_exec = (hw_f - hw_s) / 1000.0;
+    std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
+    adder.join();  // (accumulate exits the process on a failed piece)
+    feeder.join();
+    if (trace)
+        std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "spmv_hw: D2H landed (streamed)", (landed - hw_f) / 1000);
+    tr("spmv_hw: accumulation after the kernels", hw_f);
+    const double ra_exec = std::max(0.0, (timestamp_us() - hw_f) / 1000.0);
+    std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
+    std::printf("Total time  : %.6f ms elapsed\n", hw_exec + ra_exec);
+    std::fflush(stdout);
 }
 
 }  // namespace
@@ -305,6 +502,7 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
             check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
                   "warm D2H");
             check(hipStreamSynchronize(us), "warm D2H");
+            setup_streaming(h);
         }
         spmv_plan_stats st;
         spmv_plan_get_stats(h->plan, &st);
@@ -502,6 +700,13 @@ void spmv_hw(csr_hw_matrix **hw_matrix, csr_hw_vector *hw_x, csr_vector *y_fpga,
         std::fflush(stdout);
         return;
     }
+    bool streamed = units > 0 && stream_enabled();  // (read per call, like SPMV_HW_PIPELINE)
+    for (int u = 0; u < units && streamed; ++u) {
+        hw_matrix_impl *m = impl(hw_matrix[u]);
+        streamed = m->row_end == m->row_begin || (m->h_flags && sweep_can_flag_panels(*m->plan));
+    }
+    if (streamed)
+        return spmv_hw_streamed(hw_matrix, units, x, y_fpga, trace);
     // kernels of every unit (one stream per unit; units on different GPUs run concurrently)
     const double hw_s = timestamp_us();
     for (int u = 0; u < units; ++u) {
@@ -568,6 +773,13 @@ void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix)
         hw_matrix_impl *m = impl(hw_matrix[u]);
         delete m->clique;  // before the plans it borrows
         spmv_plan_destroy(m->plan);
+        if (m->copy_stream || m->h_flags) {
+            (void)hipSetDevice(m->device);
+            if (m->copy_stream)
+                (void)hipStreamDestroy(m->copy_stream);
+            if (m->h_flags)
+                (void)hipHostFree(m->h_flags);
+        }
         if (m->d_y || m->h_stage) {
             (void)hipSetDevice(m->device);
             if (m->d_y)

@@ -195,6 +195,10 @@ struct spmv_plan {
     double bin_row_limit = 0.0;        // automatic choice: give up (rc 2) when one row holds more than
                                        // this fraction of a panel's mean entries (same reason; env
                                        // SPMV_BIN_ROW_LIMIT overrides the automatic value)
+    // spmv_hw's streamed copy-back (csr_hw_wrapper.cpp): while set, the sweep kernel stores
+    // y_epoch into y_flag[panel] (host memory) once the panel's rows of y are in memory
+    uint32_t *y_flag = nullptr;
+    uint32_t y_epoch = 0;
     double locality = -1.0;    // probe result used by the automatic kernel choice
     double tuned_ms[4] = {-1.0, -1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: tiles / sweep / slices / binned ms
 
@@ -291,6 +295,9 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                 hipStream_t s);
 int probe_locality(const IndexType *d_rp, const IndexType *d_col, IndexType n, hipStream_t s, double *frac);
 int sweep_materialize_rc(spmv_plan &p);  // delta plan: rebuild the 12-byte rc words (once)
+// the plan's default launch is the packed sweep with one workgroup per panel (no combine), whose
+// workgroups can flag each panel's y as it is stored (spmv_plan::y_flag)
+bool sweep_can_flag_panels(const spmv_plan &p);
 
 // plan.cpp helpers shared with the wrapper
 int upload_staged(void *dst, const void *src, size_t bytes, hipStream_t s);  // pageable H2D, synchronous

@@ -452,7 +452,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
     const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal,
     uint32_t tail16, uint32_t nunits, const A *__restrict__ cpart, uint32_t *__restrict__ ccount,
-    uint32_t *__restrict__ cnext, uint32_t npanels, uint32_t cj)
+    uint32_t *__restrict__ cnext, uint32_t npanels, uint32_t cj, uint32_t *__restrict__ yflag, uint32_t yepoch)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -707,6 +707,16 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     __syncthreads();
     ABL_WG_STAMP(1);
     write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
+    if (yflag) {
+        // spmv_hw's streamed copy-back (plans of one piece per panel only): the panel's y is
+        // published at system scope -- every wave's stores complete, one lane's release writes
+        // the XCD L2's dirty lines back to memory -- and its flag in host memory is set to this
+        // call's epoch; the host then copies the panel's rows while the other panels still sweep
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(yflag + p, yepoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     ABL_WG_STAMP(2);
 }
 
@@ -1194,13 +1204,15 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr, \
-                       (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, 0u)
+                       (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, 0u, \
+                       p.y_flag, p.y_epoch)
     // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
 #define PKD(ST, TAIL)                                                                                 \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, gridb, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr, (uint32_t)(TAIL), \
-                       (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels, bh.rows_per_thread)
+                       (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels, bh.rows_per_thread, \
+                       p.y_flag, p.y_epoch)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         switch (p.sweep_variant) {
@@ -1274,6 +1286,12 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 
 // the variants launch_sweep_t sends to the default delta kernel (PKD(false, 0)), split plans
 // with the combine kernel: those whose launch can carry the previous step's combine
+bool sweep_can_flag_panels(const spmv_plan &p)
+{
+    return p.kernel == kKernelSweep && p.sweep_packed && !p.sweep_det && p.sweep_split == 1 && p.npanels > 0 &&
+           (p.sweep_variant == 0 || p.sweep_variant == 28);
+}
+
 bool sweep_behind_ok(const spmv_plan &p)
 {
     if (!p.sweep_packed || !p.sweep_delta || p.sweep_det || p.sweep_split < 2 || p.d_panel_cnt)

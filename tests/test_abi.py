@@ -342,7 +342,7 @@ def test_product_variant_table_matches_the_source():
 DOCUMENTED_ENV = {"SPMV_NGPUS", "SPMV_HW_MERGE", "SPMV_HW_KERNEL", "SPMV_FPGA_VF", "SPMV_FPGA_BLOCK",
                   "SPMV_SLICE_ACC", "SPMV_SWEEP_DETERMINISTIC", "SPMV_SWEEP_DELTA", "SPMV_SWEEP_XCC_BIAS",
                   "SPMV_BIN_ROW_LIMIT", "SPMV_READ_THREADS", "SPMV_HW_TRACE", "SPMV_HW_PREFAULT",
-                  "SPMV_HW_PIPELINE"}
+                  "SPMV_HW_PIPELINE", "SPMV_HW_STREAM"}
 
 
 def test_product_reads_only_the_documented_switches():

@@ -1,0 +1,100 @@
+"""spmv_hw's streamed copy-back (csr_hw_wrapper.cpp spmv_hw_streamed): on plans whose sweep runs
+one workgroup per panel, each workgroup flags its panel in host memory once the panel's rows of y
+are in memory (a system-scope release), and a feeder thread copies each piece of y (whole panels)
+while the rest still sweeps; the adding threads add every piece as it lands (accum_results'
+`+=`, csr_hw.cpp:1531-1565). The reference's three lines keep their meaning. y must be the
+oracle's (spmv_gold, csr.cpp:184-194) call after call -- the flags carry a per-call epoch, so a
+piece is never copied on the previous call's flag -- with one unit and with two units sharing the
+GPU, and identical to the unstreamed merge (SPMV_HW_STREAM=0)."""
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import spmv_hw
+
+pytestmark = pytest.mark.gpu
+
+
+def _matrix(lib, n, z, seed=4):
+    rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, z, seed=seed)
+    x = spmv_hw.gen_vector(lib, n, seed=6)
+    h = (rp.cpu().numpy().view(np.uint32), col.cpu().numpy().view(np.uint32), val.cpu().numpy(), x.cpu().numpy())
+    del rp, col, val, x
+    return h
+
+
+def _flow(lib, h_rp, h_col, h_val, h_x, calls):
+    n = len(h_rp) - 1
+    m = lib.make_csr_matrix(h_rp, h_col, h_val, n)
+    hw, bm = lib.create_csr_hw_matrix(m)
+    hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(h_x), 1, hw[0].contents.nr_cols)
+    yv = lib.make_csr_vector(np.zeros(n, h_val.dtype))
+    ys = []
+    for _ in range(calls):
+        lib.spmv_hw(hw, hx, yv, bm)
+        ys.append(np.ctypeslib.as_array(yv.values, shape=(n,)).copy())
+    lib.delete_csr_hw_matrix(hw)
+    lib.free_bitmap(bm)
+    lib.delete_csr_hw_x_vector(hx)
+    return ys
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("units", [1, 2])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_streamed_copy_back_matches_the_oracle(monkeypatch, capfd, units, dtype):
+    """A 6M-row power-law matrix (one whole-panel sweep plan per unit) through spmv_hw three
+    times: every call's y is A x added once more, within the oracle's tolerance; the trace
+    names the streamed branch; with SPMV_HW_STREAM=0 the same calls give the same bits."""
+    monkeypatch.setenv("SPMV_NGPUS", str(units))
+    monkeypatch.setenv("SPMV_HW_MERGE", "host")
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    monkeypatch.delenv("SPMV_HW_STREAM", raising=False)
+    if dtype == np.float32:  # (fp32 matrices this size take the binned kernel by default)
+        monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    lib = spmv_hw.load(dtype)
+    n, z = 6_000_000, 96_000_000
+    h = _matrix(lib, n, z)
+    ys = _flow(lib, *h, calls=3)
+    _, err = capfd.readouterr()
+    assert err.count("D2H landed (streamed)") == 3, err[-2000:]
+    ref = oracle.spmv_gold(*h) if dtype == np.float64 else oracle.spmv_fp64acc(*h)
+    tight = 1e-12 if dtype == np.float64 else 2e-6
+    assert oracle.scaled_error(*h, ref, ys[0]) <= tight
+    for k in (1, 2):  # each call adds A x once more (in the library's precision)
+        d = ys[k].astype(np.float64) - ys[k - 1].astype(np.float64)
+        assert oracle.scaled_error(*h, ref.astype(np.float64), d) <= (1e-12 if dtype == np.float64 else 1e-5)
+    monkeypatch.setenv("SPMV_HW_STREAM", "0")
+    ys0 = _flow(lib, *h, calls=1)
+    _, err = capfd.readouterr()
+    assert "streamed" not in err
+    # the sweep's LDS adds run in timing order: two runs agree to rounding, not bit for bit
+    scale = float(np.abs(ys[0].astype(np.float64)).max())
+    assert float(np.abs(ys0[0].astype(np.float64) - ys[0]).max()) <= (1e-13 if dtype == np.float64 else 1e-5) * scale
+
+
+@pytest.mark.timeout(600)
+def test_streamed_copy_back_at_headline_size(monkeypatch, capfd):
+    """Config 3's 10M/160M fp64 matrix through the drop-in with one unit (the bench's `dropin`
+    field): two rounds of whole panels, so half of y is copied while the second round sweeps.
+    y is spmv_gold's (verification 0, scaled error <= 1e-12) on every call, and the printed
+    Total is Hardware + Accumulation."""
+    monkeypatch.setenv("SPMV_NGPUS", "1")
+    monkeypatch.setenv("SPMV_HW_MERGE", "host")
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    lib = spmv_hw.load(np.float64)
+    h = _matrix(lib, 10_000_000, 160_000_000)
+    ys = _flow(lib, *h, calls=3)
+    out, err = capfd.readouterr()
+    assert err.count("D2H landed (streamed)") == 3
+    ref = oracle.spmv_gold(*h)
+    assert oracle.scaled_error(*h, ref, ys[0]) <= 1e-12
+    assert lib.verification(ref, ys[0]) == 0
+    assert oracle.scaled_error(*h, ref, ys[2] - ys[1]) <= 1e-12
+    hw = [float(v) for v in re.findall(r"Hardware execution time : ([0-9.]+)", out)]
+    ra = [float(v) for v in re.findall(r"Result accumulation time : ([0-9.]+)", out)]
+    tot = [float(v) for v in re.findall(r"Total time  : ([0-9.]+)", out)]
+    assert len(hw) == len(ra) == len(tot) == 3
+    assert all(abs(t - a - b) < 1e-3 for t, a, b in zip(tot, hw, ra))
