@@ -267,6 +267,8 @@ struct streamed_piece {
     hipEvent_t ev = nullptr;
     std::atomic<int> state{0};
     std::string err;
+    double t_ready = 0.0, t_enq = 0.0;  // (SPMV_HW_TRACE) flags all seen / copy enqueued, timestamp_us
+    bool by_flags = false;              // the flags, not the end of the kernels, released the piece
 };
 
 int wait_streamed(void *ready, std::string *err)
@@ -285,18 +287,26 @@ int wait_streamed(void *ready, std::string *err)
 // Copy each piece as soon as its panels are flagged, in landing order. A piece whose flags do
 // not all arrive is copied once its unit's kernels have ended (y is final then), so the feeder
 // ends whatever the kernel did; a failed kernel or copy marks the rest of the pieces failed.
-void feed_pieces(std::vector<streamed_piece> &pcs)
+void feed_pieces(std::vector<streamed_piece> &pcs, std::vector<double> *seen)
 {
     std::string fail;
     for (streamed_piece &pc : pcs) {
         hw_matrix_impl *m = pc.m;
         if (fail.empty()) {
             for (uint32_t spin = 0;; ++spin) {
+                if (seen && pc.m == pcs[0].m) {  // (SPMV_HW_TRACE) when each panel's flag was first seen
+                    const uint32_t P = (uint32_t)seen->size();
+                    for (uint32_t q = 0; q < P; ++q)
+                        if ((*seen)[q] == 0.0 && __atomic_load_n(&m->h_flags[q], __ATOMIC_ACQUIRE) == m->epoch)
+                            (*seen)[q] = timestamp_us();
+                }
                 bool all = true;
                 for (uint32_t q = pc.q0; q < pc.q1 && all; ++q)
                     all = __atomic_load_n(&m->h_flags[q], __ATOMIC_ACQUIRE) == m->epoch;
-                if (all)
+                if (all) {
+                    pc.by_flags = true;
                     break;
+                }
                 if (spin % 64 == 63) {  // every ~64 polls: has the unit's launch ended anyway?
                     const hipError_t q = hipStreamQuery(unit_stream(m->unit));
                     if (q == hipSuccess)
@@ -309,6 +319,7 @@ void feed_pieces(std::vector<streamed_piece> &pcs)
                 std::this_thread::yield();
             }
         }
+        pc.t_ready = timestamp_us();
         if (fail.empty()) {
             hipError_t e = hipSetDevice(m->device);
             if (e == hipSuccess)
@@ -318,6 +329,7 @@ void feed_pieces(std::vector<streamed_piece> &pcs)
                 e = hipEventRecord(pc.ev, m->copy_stream);
             if (e != hipSuccess)
                 fail = std::string("y copy: ") + hipGetErrorString(e);
+            pc.t_enq = timestamp_us();
         }
         if (!fail.empty()) {
             pc.err = fail;
@@ -415,7 +427,8 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
             die(std::string("spmv_hw: ") + spmv_hw_last_error());
     }
     tr("spmv_hw: launches", hw_s);
-    std::thread feeder(feed_pieces, std::ref(pcs));
+    std::vector<double> seen(trace && !cuts.empty() ? cuts[0].first->panel_rows.size() - 1 : 0, 0.0);
+    std::thread feeder(feed_pieces, std::ref(pcs), trace ? &seen : nullptr);
     double landed = 0.0;
     std::thread adder([&] { landed = accumulate(parts, wait_streamed); });
     for (int u = 0; u < units; ++u) {
@@ -427,8 +440,22 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
     std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
     adder.join();  // (accumulate exits the process on a failed piece)
     feeder.join();
-    if (trace)
+    if (trace) {
         std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "spmv_hw: D2H landed (streamed)", (landed - hw_f) / 1000);
+        std::vector<double> t;
+        for (double v : seen)
+            if (v > 0.0)
+                t.push_back((v - hw_s) / 1000);
+        std::sort(t.begin(), t.end());
+        if (!t.empty())
+            std::fprintf(stderr, "spmv_hw trace:   unit 0: %zu of %zu panel flags seen before the feeder moved on; "
+                                 "first %.3f, median %.3f, last %.3f ms after the launch\n",
+                         t.size(), seen.size(), t.front(), t[t.size() / 2], t.back());
+        for (const streamed_piece &pc : pcs)  // when each piece was released and its copy enqueued, from the launch
+            std::fprintf(stderr, "spmv_hw trace:   piece unit %d panels [%u, %u) ready %.3f ms (%s), enqueued %.3f ms\n",
+                         pc.m->unit, pc.q0, pc.q1, (pc.t_ready - hw_s) / 1000, pc.by_flags ? "flags" : "kernel end",
+                         (pc.t_enq - hw_s) / 1000);
+    }
     tr("spmv_hw: accumulation after the kernels", hw_f);
     const double ra_exec = std::max(0.0, (timestamp_us() - hw_f) / 1000.0);
     std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);
