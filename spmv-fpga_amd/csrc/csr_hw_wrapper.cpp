@@ -258,7 +258,7 @@ int wait_event(void *ready, std::string *err)
 }
 
 // One piece of a streamed copy-back: rows [b, e) of unit m's slice = its panels [q0, q1). The
-// feeder thread records `ev` after the piece's copy once every panel of it is flagged; until
+// calling thread records `ev` after the piece's copy once every panel of it is flagged; until
 // then an adding thread waits on `state` (0 pending, 1 copy enqueued, -1 failed).
 struct streamed_piece {
     hw_matrix_impl *m = nullptr;
@@ -284,39 +284,60 @@ int wait_streamed(void *ready, std::string *err)
     return wait_event(pc->ev, err);
 }
 
-// Copy each piece as soon as its panels are flagged, in landing order. A piece whose flags do
-// not all arrive is copied once its unit's kernels have ended (y is final then), so the feeder
-// ends whatever the kernel did; a failed kernel or copy marks the rest of the pieces failed.
-void feed_pieces(std::vector<streamed_piece> &pcs, std::vector<double> *seen)
+// Copy each piece as soon as its panels are flagged, in landing order, on the calling thread --
+// the only thread that asks about the units' kernel streams (a runtime call on a stream another
+// thread is synchronising on waits for that synchronisation: the flags would be seen at the end
+// of the kernel only). A piece whose flags do not all arrive is copied once its unit's kernels
+// have ended (y is final then), so this returns whatever the kernel did; a failed kernel or copy
+// marks the rest of the pieces failed. Returns when every piece's copy is enqueued and every
+// unit's kernels have ended, and when (timestamp_us) the last of them was seen to end.
+double feed_pieces(std::vector<streamed_piece> &pcs, const std::vector<hw_matrix_impl *> &us,
+                   std::vector<double> *seen)
 {
     std::string fail;
+    std::vector<double> ended(us.size(), 0.0);
+    auto poll_units = [&]() {  // has each unit's launch ended? (first time seen, timestamp_us)
+        bool all = true;
+        for (size_t k = 0; k < us.size(); ++k) {
+            if (ended[k] > 0.0)
+                continue;
+            const hipError_t q = hipStreamQuery(unit_stream(us[k]->unit));
+            if (q == hipSuccess) {
+                ended[k] = timestamp_us();
+            } else {
+                all = false;
+                if (q != hipErrorNotReady && fail.empty())
+                    fail = std::string("spmv kernels: ") + hipGetErrorString(q);
+            }
+        }
+        return all;
+    };
+    auto unit_ended = [&](const hw_matrix_impl *m) {
+        for (size_t k = 0; k < us.size(); ++k)
+            if (us[k] == m)
+                return ended[k] > 0.0;
+        return true;
+    };
     for (streamed_piece &pc : pcs) {
         hw_matrix_impl *m = pc.m;
-        if (fail.empty()) {
-            for (uint32_t spin = 0;; ++spin) {
-                if (seen && pc.m == pcs[0].m) {  // (SPMV_HW_TRACE) when each panel's flag was first seen
-                    const uint32_t P = (uint32_t)seen->size();
-                    for (uint32_t q = 0; q < P; ++q)
-                        if ((*seen)[q] == 0.0 && __atomic_load_n(&m->h_flags[q], __ATOMIC_ACQUIRE) == m->epoch)
-                            (*seen)[q] = timestamp_us();
-                }
-                bool all = true;
-                for (uint32_t q = pc.q0; q < pc.q1 && all; ++q)
-                    all = __atomic_load_n(&m->h_flags[q], __ATOMIC_ACQUIRE) == m->epoch;
-                if (all) {
-                    pc.by_flags = true;
+        for (uint32_t spin = 0; fail.empty(); ++spin) {
+            if (seen && pc.m == pcs[0].m) {  // (SPMV_HW_TRACE) when each panel's flag was first seen
+                const uint32_t P = (uint32_t)seen->size();
+                for (uint32_t q = 0; q < P; ++q)
+                    if ((*seen)[q] == 0.0 && __atomic_load_n(&m->h_flags[q], __ATOMIC_ACQUIRE) == m->epoch)
+                        (*seen)[q] = timestamp_us();
+            }
+            bool all = true;
+            for (uint32_t q = pc.q0; q < pc.q1 && all; ++q)
+                all = __atomic_load_n(&m->h_flags[q], __ATOMIC_ACQUIRE) == m->epoch;
+            if (all) {
+                pc.by_flags = true;
+                break;
+            }
+            if (spin % 16 == 15) {
+                poll_units();
+                if (unit_ended(m))
                     break;
-                }
-                if (spin % 64 == 63) {  // every ~64 polls: has the unit's launch ended anyway?
-                    const hipError_t q = hipStreamQuery(unit_stream(m->unit));
-                    if (q == hipSuccess)
-                        break;
-                    if (q != hipErrorNotReady) {
-                        fail = std::string("spmv kernels: ") + hipGetErrorString(q);
-                        break;
-                    }
-                }
-                std::this_thread::yield();
             }
         }
         pc.t_ready = timestamp_us();
@@ -338,6 +359,11 @@ void feed_pieces(std::vector<streamed_piece> &pcs, std::vector<double> *seen)
             pc.state.store(1, std::memory_order_release);
         }
     }
+    while (fail.empty() && !poll_units())
+        std::this_thread::yield();
+    if (!fail.empty())
+        die(fail);
+    return *std::max_element(ended.begin(), ended.end());
 }
 
 // accum_results' '+=' of the landed pieces into the caller's y (spmv_host.hpp, host.cpp) on up
@@ -362,8 +388,8 @@ double accumulate(const std::vector<add_part> &parts, int (*wait)(void *, std::s
 }
 
 // spmv_hw with the host merge on plans whose sweep flags each panel (csr_hw_wrapper.cpp:193-288):
-// every unit's kernel is launched with this call's epoch; a feeder thread copies each piece of
-// y (8 pieces in all, whole panels each) as soon as its panels are flagged, and the adding
+// every unit's kernel is launched with this call's epoch; the calling thread copies each piece
+// of y (8 pieces in all, whole panels each) as soon as its panels are flagged, and the adding
 // threads add every piece as soon as it landed -- so the PCIe copy-back and the host '+=' run
 // while the SpMV still sweeps, instead of after it. The printed times keep the reference's
 // meaning: "Hardware execution" ends when every unit's kernels have ended, "Result accumulation"
@@ -428,18 +454,15 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
     }
     tr("spmv_hw: launches", hw_s);
     std::vector<double> seen(trace && !cuts.empty() ? cuts[0].first->panel_rows.size() - 1 : 0, 0.0);
-    std::thread feeder(feed_pieces, std::ref(pcs), trace ? &seen : nullptr);
+    std::vector<hw_matrix_impl *> us;
+    for (auto &c : cuts)
+        us.push_back(c.first);
     double landed = 0.0;
     std::thread adder([&] { landed = accumulate(parts, wait_streamed); });
-    for (int u = 0; u < units; ++u) {
-        check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
-        check(hipStreamSynchronize(unit_stream(u)), "spmv kernels");
-    }
-    const double hw_f = timestamp_us();
+    const double hw_f = us.empty() ? timestamp_us() : feed_pieces(pcs, us, trace ? &seen : nullptr);
     const double hw_exec = (hw_f - hw_s) / 1000.0;
     std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
     adder.join();  // (accumulate exits the process on a failed piece)
-    feeder.join();
     if (trace) {
         std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "spmv_hw: D2H landed (streamed)", (landed - hw_f) / 1000);
         std::vector<double> t;
@@ -448,7 +471,7 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
                 t.push_back((v - hw_s) / 1000);
         std::sort(t.begin(), t.end());
         if (!t.empty())
-            std::fprintf(stderr, "spmv_hw trace:   unit 0: %zu of %zu panel flags seen before the feeder moved on; "
+            std::fprintf(stderr, "spmv_hw trace:   unit 0: %zu of %zu panel flags seen while the pieces were fed; "
                                  "first %.3f, median %.3f, last %.3f ms after the launch\n",
                          t.size(), seen.size(), t.front(), t[t.size() / 2], t.back());
         for (const streamed_piece &pc : pcs)  // when each piece was released and its copy enqueued, from the launch
