@@ -39,6 +39,19 @@ __global__ void k_raise(uint32_t *flag, int mode, uint64_t hold_ticks)
         __builtin_amdgcn_s_sleep(8);
 }
 
+// occupies every CU (one 1024-thread workgroup with 128 KiB of LDS each) for hold_ticks
+__global__ __launch_bounds__(1024) void k_hog(uint64_t hold_ticks, float *sink)
+{
+    extern __shared__ float lds[];
+    lds[threadIdx.x] = float(threadIdx.x);
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < hold_ticks)
+        __builtin_amdgcn_s_sleep(8);
+    __syncthreads();
+    if (lds[(threadIdx.x + 1) % 1024] < -1.0f)
+        sink[0] = 1.0f;
+}
+
 static double now_us()
 {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -102,6 +115,44 @@ int main(int argc, char **argv)
             CK(hipDeviceSynchronize());
             std::printf("{\"mode\": %d, \"rep\": %d, \"seen_us\": %.1f, \"kernel_end_us\": %.1f, \"seen_before_end\": %s}\n",
                         mode, r, seen, end, seen >= 0.0 && seen < end - 50.0 ? "true" : "false");
+            std::fflush(stdout);
+        }
+    }
+    // mode 4: a 40 MB device -> pinned host copy on a second stream while every CU is held by a
+    // kernel for 1 ms: does the copy finish during the kernel (a copy engine) or after it (a
+    // copy kernel that waits for CUs)? Copy alone for reference.
+    {
+        const size_t bytes = 40u << 20;
+        char *d_big = nullptr, *h_big = nullptr;
+        float *sink = nullptr;
+        CK(hipMalloc((void **)&d_big, bytes));
+        CK(hipMalloc((void **)&sink, 64));
+        CK(hipHostMalloc((void **)&h_big, bytes, hipHostMallocDefault));
+        int cus = 0;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        CK(hipMemcpyAsync(h_big, d_big, bytes, hipMemcpyDeviceToHost, cs));
+        CK(hipDeviceSynchronize());
+        for (int r = 0; r < reps; ++r) {
+            double t0 = now_us();
+            CK(hipMemcpyAsync(h_big, d_big, bytes, hipMemcpyDeviceToHost, cs));
+            CK(hipStreamSynchronize(cs));
+            const double alone = now_us() - t0;
+            CK(hipDeviceSynchronize());
+            t0 = now_us();
+            hipLaunchKernelGGL(k_hog, dim3(cus), dim3(1024), 128 * 1024, ks, (uint64_t)100000, sink);
+            CK(hipGetLastError());
+            CK(hipMemcpyAsync(h_big, d_big, bytes, hipMemcpyDeviceToHost, cs));
+            CK(hipEventRecord(ev, cs));
+            double copy_done = -1.0, end = -1.0;
+            while (copy_done < 0.0 || end < 0.0) {
+                if (copy_done < 0.0 && hipEventQuery(ev) == hipSuccess)
+                    copy_done = now_us() - t0;
+                if (end < 0.0 && hipStreamQuery(ks) == hipSuccess)
+                    end = now_us() - t0;
+            }
+            std::printf("{\"mode\": 4, \"rep\": %d, \"copy_alone_us\": %.1f, \"copy_done_us\": %.1f, "
+                        "\"hog_end_us\": %.1f, \"copy_during_hog\": %s}\n",
+                        r, alone, copy_done, end, copy_done < end ? "true" : "false");
             std::fflush(stdout);
         }
     }
