@@ -156,5 +156,34 @@ int main(int argc, char **argv)
             std::fflush(stdout);
         }
     }
+    // mode 5: 80 MB device -> pinned host in 8 pieces on 1, 2 or 4 streams (copy engines in
+    // parallel?), and as one copy; ms of the whole transfer
+    {
+        const size_t bytes = 80u << 20, piece = bytes / 8;
+        char *d_big = nullptr, *h_big = nullptr;
+        CK(hipMalloc((void **)&d_big, bytes));
+        CK(hipHostMalloc((void **)&h_big, bytes, hipHostMallocDefault));
+        hipStream_t ss[4];
+        for (auto &x : ss)
+            CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        for (int k = 0; k < 4; ++k)  // warm every stream's copy path
+            CK(hipMemcpyAsync(h_big, d_big, bytes, hipMemcpyDeviceToHost, ss[k]));
+        CK(hipDeviceSynchronize());
+        for (int r = 0; r < reps; ++r) {
+            for (int nst : {0, 1, 2, 4}) {
+                const double t0 = now_us();
+                if (nst == 0) {
+                    CK(hipMemcpyAsync(h_big, d_big, bytes, hipMemcpyDeviceToHost, ss[0]));
+                } else {
+                    for (int k = 0; k < 8; ++k)
+                        CK(hipMemcpyAsync(h_big + k * piece, d_big + k * piece, piece, hipMemcpyDeviceToHost, ss[k % nst]));
+                }
+                CK(hipDeviceSynchronize());
+                std::printf("{\"mode\": 5, \"rep\": %d, \"streams\": %d, \"pieces\": %d, \"ms\": %.3f, \"GBps\": %.1f}\n",
+                            r, nst ? nst : 1, nst ? 8 : 1, (now_us() - t0) / 1000, bytes / (now_us() - t0) / 1000);
+                std::fflush(stdout);
+            }
+        }
+    }
     return 0;
 }
