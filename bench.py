@@ -479,9 +479,13 @@ def full_parity(h):
     nz = yr != 0
     rel = float(np.max(np.abs(yg64[nz] - yr[nz]) / np.abs(yr[nz]))) if nz.any() else 0.0
     tol = 1e-6 if ref.dtype == np.float64 else 1e-4
+    # the north star's gate is the componentwise-scaled error; in fp64 the reference's own check
+    # (verification: |dy| < 1e-5 absolute, csr_hw.cpp:1571-1590) must pass too. In fp32 that
+    # absolute bound is below the rounding of |y| ~ 1e2 (spmv_gold sums in fp32, the kernels in
+    # fp64), so its count is reported only
     parity = {"scope": f"full matrix ({n} rows) vs spmv_gold", "rows_checked": n, "max_scaled_err": err, "tol": tol,
               "max_rel_err": rel, "ref_abs_1e-5_errors": abs_errors,
-              "pass": bool(err <= tol and abs_errors == 0)}
+              "pass": bool(err <= tol and (abs_errors == 0 or ref.dtype != np.float64))}
     return parity, ref, sw_ms
 
 
@@ -586,7 +590,7 @@ def run_dropin(args, units, merge, ref, sw_ms, timeout):
         except OSError:
             pass
     js = [ln[len("DROPIN_JSON "):] for ln in out.splitlines() if ln.startswith("DROPIN_JSON ")]
-    if p.returncode not in (0, 3) or not js:
+    if p.returncode != 0 or not js:
         return {"error": f"drop-in child exit status {p.returncode}: {(err or out)[-400:]}", "pass": None}
     d = json.loads(js[-1])
     hw = _ref_lines(out, "Hardware execution time")
@@ -613,8 +617,10 @@ def run_dropin(args, units, merge, ref, sw_ms, timeout):
            "max_rel_diff_vs_spmv_gold": max(c["max_rel_diff"] for c in calls), "tol": tol,
            "storage_mb": d["storage_mb"], "csr_mb": d["csr_mb"],
            "child_wall_s": round(time.perf_counter() - t0, 2)}
-    res["pass"] = bool(p.returncode == 0 and all(v == 0 for v in res["verification"])
-                       and res["max_rel_diff_vs_spmv_gold"] <= tol)
+    # fp64: every call's verification is 0 (main.cpp:77-82); fp32: the normwise difference only
+    # (the absolute 1e-5 bound is below fp32 rounding of this y; see full_parity)
+    res["pass"] = bool(res["max_rel_diff_vs_spmv_gold"] <= tol
+                       and (args.dtype != "f64" or all(v == 0 for v in res["verification"])))
     if os.environ.get("SPMV_BENCH_INJECT") == "dropin":
         res["verification"][0], res["pass"] = 1, False  # test hook: a failed drop-in verification
     return res
