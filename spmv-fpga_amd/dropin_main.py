@@ -64,7 +64,22 @@ def host_matrix(lib, args):
     return h
 
 
+def _die_with_parent():
+    """This process is SIGKILLed when the bench rank that started it dies (Linux prctl
+    PR_SET_PDEATHSIG, set from here: the rank has threads, so no preexec hook there), so a rank
+    killed at a deadline leaves no drop-in run holding the node's GPUs."""
+    parent = os.getppid()
+    try:
+        import signal
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGKILL, 0, 0, 0)
+    except Exception:
+        return
+    if os.getppid() != parent:  # the parent was already gone
+        os._exit(1)
+
+
 def main(argv=None):
+    _die_with_parent()
     args = parse(argv)
     os.environ["SPMV_HW_MERGE"] = args.merge  # read by create_csr_hw_matrix
     import spmv_hw
