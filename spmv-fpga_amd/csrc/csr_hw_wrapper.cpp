@@ -111,6 +111,8 @@ struct hw_matrix_impl {
     // the pieces' copies run on while the kernel still sweeps
     uint32_t *h_flags = nullptr;
     uint32_t *d_flags = nullptr;
+    ValueType *h_direct = nullptr;  // (tools build, SPMV_HW_DIRECT=1) y stored by the sweep over PCIe
+    ValueType *d_direct = nullptr;
     uint32_t epoch = 0;
     std::vector<uint32_t> panel_rows;
     hipStream_t copy_stream = nullptr;
@@ -211,6 +213,11 @@ void setup_streaming(hw_matrix_impl *m)
     check(hipHostGetDevicePointer((void **)&m->d_flags, m->h_flags, 0), "hipHostGetDevicePointer(panel flags)");
     check(hipStreamCreateWithFlags(&m->copy_stream, hipStreamNonBlocking), "hipStreamCreate");
     const uint64_t rows = m->row_end - m->row_begin;
+    if (ablation_env("SPMV_HW_DIRECT")) {  // the measurement form: y straight into host memory
+        check(hipHostMalloc((void **)&m->h_direct, rows * sizeof(ValueType), hipHostMallocCoherent | hipHostMallocMapped),
+              "hipHostMalloc(direct y)");
+        check(hipHostGetDevicePointer((void **)&m->d_direct, m->h_direct, 0), "hipHostGetDevicePointer(direct y)");
+    }
     check(hipMemcpyAsync(m->h_stage, m->d_y, rows * sizeof(ValueType), hipMemcpyDeviceToHost, m->copy_stream),
           "warm D2H");
     check(hipStreamSynchronize(m->copy_stream), "warm D2H");
@@ -281,7 +288,7 @@ int wait_streamed(void *ready, std::string *err)
         *err = pc->err;
         return 1;
     }
-    return wait_event(pc->ev, err);
+    return pc->ev ? wait_event(pc->ev, err) : 0;  // (direct form: the flags were the landing)
 }
 
 // Copy each piece as soon as its panels are flagged, in landing order, on the calling thread --
@@ -341,7 +348,11 @@ double feed_pieces(std::vector<streamed_piece> &pcs, const std::vector<hw_matrix
             }
         }
         pc.t_ready = timestamp_us();
-        if (fail.empty()) {
+        if (fail.empty() && m->plan->y_host) {
+            // direct form: the rows are in host memory already (a piece released by the kernel's
+            // end is too: the end of the kernel publishes every store at system scope)
+            pc.ev = nullptr;
+        } else if (fail.empty()) {
             hipError_t e = hipSetDevice(m->device);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(m->h_stage + pc.b, m->d_y + pc.b, (pc.e - pc.b) * sizeof(ValueType),
@@ -433,9 +444,15 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
             pc.ev = m->done.get(j);
         }
     }
+    // (tools build) SPMV_HW_DIRECT=1: every unit's sweep stores y straight into host memory
+    const char *de = ablation_env("SPMV_HW_DIRECT");
+    bool direct = de && de[0] == '1';
+    for (auto &c : cuts)
+        direct = direct && c.first->d_direct;
     std::vector<add_part> parts(n);
     for (size_t k = 0; k < n; ++k)
-        parts[k] = {y_fpga->values + pcs[k].m->row_begin + pcs[k].b, pcs[k].m->h_stage + pcs[k].b, pcs[k].e - pcs[k].b,
+        parts[k] = {y_fpga->values + pcs[k].m->row_begin + pcs[k].b,
+                    (direct ? pcs[k].m->h_direct : pcs[k].m->h_stage) + pcs[k].b, pcs[k].e - pcs[k].b,
                     static_cast<void *>(&pcs[k])};
 
     const double hw_s = timestamp_us();
@@ -447,6 +464,7 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
             m->epoch = 1;
         m->plan->y_flag = m->d_flags;
         m->plan->y_epoch = m->epoch;
+        m->plan->y_host = direct ? m->d_direct : nullptr;
         const int rc = spmv_plan_run(m->plan, x->per_device[m->device], m->d_y, unit_stream(u));
         m->plan->y_flag = nullptr;
         if (rc)
@@ -460,6 +478,8 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
     double landed = 0.0;
     std::thread adder([&] { landed = accumulate(parts, wait_streamed); });
     const double hw_f = us.empty() ? timestamp_us() : feed_pieces(pcs, us, trace ? &seen : nullptr);
+    for (hw_matrix_impl *m : us)
+        m->plan->y_host = nullptr;
     const double hw_exec = (hw_f - hw_s) / 1000.0;
     std::printf("Hardware execution time : %.6f ms elapsed\n", hw_exec);
     adder.join();  // (accumulate exits the process on a failed piece)
@@ -829,6 +849,8 @@ void delete_csr_hw_matrix(csr_hw_matrix **hw_matrix)
                 (void)hipStreamDestroy(m->copy_stream);
             if (m->h_flags)
                 (void)hipHostFree(m->h_flags);
+            if (m->h_direct)
+                (void)hipHostFree(m->h_direct);
         }
         if (m->d_y || m->h_stage) {
             (void)hipSetDevice(m->device);

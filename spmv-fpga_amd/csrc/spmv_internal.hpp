@@ -199,6 +199,8 @@ struct spmv_plan {
     // y_epoch into y_flag[panel] (host memory) once the panel's rows of y are in memory
     uint32_t *y_flag = nullptr;
     uint32_t y_epoch = 0;
+    ValueType *y_host = nullptr;  // (tools build, SPMV_HW_DIRECT=1) the sweep stores y here instead
+                                  // of d_y: mapped pinned host memory
     double locality = -1.0;    // probe result used by the automatic kernel choice
     double tuned_ms[4] = {-1.0, -1.0, -1.0, -1.0};  // SPMV_HW_KERNEL=tune: tiles / sweep / slices / binned ms
 

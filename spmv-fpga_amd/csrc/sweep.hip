@@ -452,7 +452,8 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
     const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal,
     uint32_t tail16, uint32_t nunits, const A *__restrict__ cpart, uint32_t *__restrict__ ccount,
-    uint32_t *__restrict__ cnext, uint32_t npanels, uint32_t cj, uint32_t *__restrict__ yflag, uint32_t yepoch)
+    uint32_t *__restrict__ cnext, uint32_t npanels, uint32_t cj, uint32_t *__restrict__ yflag, uint32_t yepoch,
+    V *__restrict__ yhost)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -706,7 +707,10 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         lds_add(&ylds[R], sink);
     __syncthreads();
     ABL_WG_STAMP(1);
-    write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
+    // (yhost: the tools build's direct form of spmv_hw's copy-back -- the panel's y stored straight
+    // into pinned host memory over PCIe instead of device memory; plans of one piece per panel)
+    write_panel<V, T, A>(ylds, R, (yhost ? yhost : y) + r0, pieces, part, stride, panel_unit[p],
+                         pcnt ? pcnt + p : nullptr);
     if (yflag) {
         // spmv_hw's streamed copy-back (plans of one piece per panel only): the panel's y is
         // published at system scope -- every wave's stores complete, one lane's release writes
@@ -1205,14 +1209,14 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr, \
                        (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, 0u, \
-                       p.y_flag, p.y_epoch)
+                       p.y_flag, p.y_epoch, p.y_host)
     // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
 #define PKD(ST, TAIL)                                                                                 \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, gridb, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr, (uint32_t)(TAIL), \
                        (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels, bh.rows_per_thread, \
-                       p.y_flag, p.y_epoch)
+                       p.y_flag, p.y_epoch, p.y_host)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         switch (p.sweep_variant) {

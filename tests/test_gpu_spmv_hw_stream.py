@@ -13,6 +13,7 @@ import pytest
 
 import oracle
 import spmv_hw
+from conftest import tools_env
 
 pytestmark = pytest.mark.gpu
 
@@ -98,3 +99,22 @@ def test_streamed_copy_back_at_headline_size(monkeypatch, capfd):
     tot = [float(v) for v in re.findall(r"Total time  : ([0-9.]+)", out)]
     assert len(hw) == len(ra) == len(tot) == 3
     assert all(abs(t - a - b) < 1e-3 for t, a, b in zip(tot, hw, ra))
+
+
+@pytest.mark.timeout(300)
+def test_direct_form_of_the_tools_build(monkeypatch, capfd):
+    """The tools build's direct form (SPMV_HW_DIRECT=1, a measurement variant): the sweep stores
+    each panel's y straight into pinned host memory over PCIe and flags it; the host adds from
+    there with no copy. y is the oracle's on every call."""
+    monkeypatch.setenv("SPMV_NGPUS", "1")
+    monkeypatch.setenv("SPMV_HW_MERGE", "host")
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    tools_env(monkeypatch, "SPMV_HW_DIRECT", "1")
+    lib = spmv_hw.load(np.float64)
+    h = _matrix(lib, 6_000_000, 96_000_000)
+    ys = _flow(lib, *h, calls=3)
+    _, err = capfd.readouterr()
+    assert err.count("D2H landed (streamed)") == 3
+    ref = oracle.spmv_gold(*h)
+    assert oracle.scaled_error(*h, ref, ys[0]) <= 1e-12
+    assert oracle.scaled_error(*h, ref, ys[2] - ys[1]) <= 1e-12

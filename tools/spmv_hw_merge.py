@@ -31,7 +31,7 @@ import torch  # noqa: E402
 import spmv_hw  # noqa: E402
 
 KNOBS = {"pipe": "SPMV_HW_PIPELINE", "pieces": "SPMV_HW_PIECES", "split": "SPMV_HW_ADD_SPLIT",
-         "threads": "SPMV_HW_ADD_THREADS", "stream": "SPMV_HW_STREAM"}
+         "threads": "SPMV_HW_ADD_THREADS", "stream": "SPMV_HW_STREAM", "direct": "SPMV_HW_DIRECT"}
 LINES = {"hw_ms": "Hardware execution time", "accum_ms": "Result accumulation time", "total_ms": "Total time"}
 
 
