@@ -33,7 +33,12 @@ Multi-GPU (--gpus N, one process per GPU, torch.distributed over RCCL):
 Extra JSON fields: roofline (dominant kernel of the plan: k_spmv_sweep_packed for the power-law
 matrix, k_spmv_tiles for the banded one; HIP events on its launch stream),
 cpu_baseline (the oracle's restatement of spmv_gold, 1 thread, on the host of the GPU box),
-parity (full-size componentwise-scaled error vs that oracle run),
+parity (full-size componentwise-scaled error vs that oracle run; mandatory at every N: a failed
+or missing check prints value null / valid false and exits 3), dropin (the drop-in boundary
+itself: create_csr_hw_matrix -> spmv_hw -> verification in a child process, the reference's
+"Matrix read", "Hardware execution", "Result accumulation" and "Total" times; at N > 1 rank 0
+runs it with N units merged by the library's RCCL reduce), value_e2e (2 nnz / (SpMV step +
+the exchange that completes y); = value at N = 1),
 lds_xtiles (power-law, 1 GPU: the same matrix through kernel 4, the reference's dataflow with a
 block of x in LDS per workgroup -- the technique BASELINE configs 3/5 name -- timed beside the
 headline kernel), binned (power-law, 1 GPU: the same matrix through kernel 6, the two-pass
