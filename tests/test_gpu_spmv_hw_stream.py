@@ -118,3 +118,42 @@ def test_direct_form_of_the_tools_build(monkeypatch, capfd):
     ref = oracle.spmv_gold(*h)
     assert oracle.scaled_error(*h, ref, ys[0]) <= 1e-12
     assert oracle.scaled_error(*h, ref, ys[2] - ys[1]) <= 1e-12
+
+
+@pytest.mark.timeout(300)
+def test_streamed_copy_back_with_empty_rows(monkeypatch, capfd):
+    """Empty rows (20 %, in runs and alone) and a last row that is empty: every row of y comes
+    back through the flagged panels -- the empty ones as 0 -- and matches spmv_gold (here with
+    a y_fpga that starts non-zero, since spmv_hw adds)."""
+    monkeypatch.setenv("SPMV_NGPUS", "1")
+    monkeypatch.setenv("SPMV_HW_MERGE", "host")
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    rng = np.random.default_rng(21)
+    n = 6_000_000
+    lens = rng.poisson(16, n)
+    lens[rng.random(n) < 0.2] = 0
+    lens[1000:50_000] = 0  # a run of empty rows longer than a panel
+    lens[-1] = 0
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    z = int(rp[-1])
+    col = rng.integers(0, n, z, dtype=np.uint32)
+    val = rng.uniform(-1, 1, z)
+    x = rng.uniform(0, 1, n)
+    rp = rp.astype(np.uint32)
+    lib = spmv_hw.load(np.float64)
+    m = lib.make_csr_matrix(rp, col, val, n)
+    hw, bm = lib.create_csr_hw_matrix(m)
+    hx = lib.create_csr_hw_x_vector(lib.make_csr_vector(x), 1, hw[0].contents.nr_cols)
+    y0 = rng.uniform(-1, 1, n)
+    yv = lib.make_csr_vector(y0.copy())
+    lib.spmv_hw(hw, hx, yv, bm)
+    y = np.ctypeslib.as_array(yv.values, shape=(n,)).copy()
+    lib.delete_csr_hw_matrix(hw)
+    lib.free_bitmap(bm)
+    lib.delete_csr_hw_x_vector(hx)
+    _, err = capfd.readouterr()
+    assert "D2H landed (streamed)" in err, err[-2000:]
+    ref = oracle.spmv_gold(rp, col, val, x)
+    assert oracle.scaled_error(rp, col, val, x, ref, y - y0) <= 1e-12
+    assert np.array_equal(y[lens == 0], y0[lens == 0])  # empty rows: y_fpga += 0
