@@ -1,3 +1,7 @@
+"""Traces spmv_hw's streamed copy-back on the 10M/160M fp64 matrix (one unit, host merge,
+SPMV_HW_TRACE=1): four calls, each printing when every piece of y was released (by its panels'
+flags or by the end of the kernel) and its copy enqueued, and when the panel flags were first
+seen (profiles/r06f_spmv_hw_stream_trace.txt). Measurement tool, not product code."""
 import os, sys
 sys.path.insert(0, "spmv-fpga_amd")
 import numpy as np, torch, spmv_hw
