@@ -575,7 +575,7 @@ def run_dropin(args, units, merge, ref, sw_ms, timeout):
         np.save(path, ref)
         cmd = [sys.executable, os.path.join(ROOT, "spmv-fpga_amd", "dropin_main.py"), "--workload", args.workload,
                "--dtype", args.dtype, "--rows", str(n), "--nnz", str(z), "--units", str(units), "--merge", merge,
-               "--reps", str(max(1, args.dropin_reps)), "--ref", path]
+               "--reps", str(max(1, args.dropin_reps)), "--ref", path, "--ab-unstreamed", str(max(1, args.dropin_reps))]
         env = {k: v for k, v in os.environ.items()
                if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR",
                             "MASTER_PORT", STAGE_FD_ENV, "SPMV_NGPUS", "SPMV_HW_MERGE")}
@@ -598,9 +598,11 @@ def run_dropin(args, units, merge, ref, sw_ms, timeout):
     if p.returncode != 0 or not js:
         return {"error": f"drop-in child exit status {p.returncode}: {(err or out)[-400:]}", "pass": None}
     d = json.loads(js[-1])
-    hw = _ref_lines(out, "Hardware execution time")
-    ra = _ref_lines(out, "Result accumulation time")
-    tot = _ref_lines(out, "Total time")
+    main_out, _, ab_out = out.partition("DROPIN_AB_UNSTREAMED")
+    hw = _ref_lines(main_out, "Hardware execution time")
+    ra = _ref_lines(main_out, "Result accumulation time")
+    tot = _ref_lines(main_out, "Total time")
+    ab_tot = _ref_lines(ab_out, "Total time")
     calls = d["calls"]
     if not (len(hw) == len(ra) == len(tot) == len(calls) >= 1):
         return {"error": f"drop-in child printed {len(hw)}/{len(ra)}/{len(tot)} timing lines for "
@@ -618,6 +620,9 @@ def run_dropin(args, units, merge, ref, sw_ms, timeout):
                            "spmv_hw_wall": [c["wall_ms"] for c in calls]},
            "total_gflops_median": round(2.0 * d["nnz"] / (med(tot) * 1e-3) / 1e9, 3) if med(tot) > 0 else None,
            "software_execution_ms": round(sw_ms, 3) if sw_ms else None,
+           # the same matrix's calls with SPMV_HW_STREAM=0 (y copied back after the kernel; the
+           # streamed copy-back applies to one-piece-per-panel sweep plans with the host merge)
+           "unstreamed_total_ms": {"median": med(ab_tot), "calls": ab_tot} if ab_tot else None,
            "verification": [c["verification"] for c in calls],
            "max_rel_diff_vs_spmv_gold": max(c["max_rel_diff"] for c in calls), "tol": tol,
            "storage_mb": d["storage_mb"], "csr_mb": d["csr_mb"],

@@ -44,6 +44,9 @@ def parse(argv=None):
     ap.add_argument("--merge", choices=["host", "gather", "reduce"], default="host")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ref", required=True, help=".npy of the software y (spmv_gold of the same matrix)")
+    ap.add_argument("--ab-unstreamed", type=int, default=0,
+                    help="then this many more calls with SPMV_HW_STREAM=0 (the copy after the kernel), "
+                         "printed after a line DROPIN_AB_UNSTREAMED")
     return ap.parse_args(argv)
 
 
@@ -121,6 +124,16 @@ def main(argv=None):
         scale = max(float(np.abs(ref).max()), 1e-300) if n else 1.0
         diff = float(np.abs(y_view.astype(np.float64) - ref).max() / scale) if n else 0.0
         calls.append({"wall_ms": round(wall_ms, 4), "verification": status, "max_rel_diff": diff})
+
+    if args.ab_unstreamed > 0:  # the same calls with the copy-back after the kernel
+        os.environ["SPMV_HW_STREAM"] = "0"  # (read per call)
+        flush()
+        print("DROPIN_AB_UNSTREAMED", flush=True)
+        for _ in range(args.ab_unstreamed):
+            y_view.fill(0)
+            lib.spmv_hw(hw, hx, y_fpga, bm)
+            flush()
+        os.environ.pop("SPMV_HW_STREAM", None)
 
     units = lib.units()
     mem = sum(lib.storage_overhead(hw[u]) for u in range(units))

@@ -62,6 +62,7 @@ def test_bench_one_gpu_line():
         assert di[k] > 0, (k, di)
     assert abs(di["total_ms"] - di["hardware_execution_ms"] - di["result_accumulation_ms"]) < 1e-3
     assert di["software_execution_ms"] > 0 and di["storage_mb"] > 0
+    assert len(di["unstreamed_total_ms"]["calls"]) == 5 and di["unstreamed_total_ms"]["median"] > 0
 
 
 @pytest.mark.parametrize("scaling", ["strong", "weak"])
