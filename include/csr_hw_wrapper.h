@@ -116,7 +116,10 @@ typedef struct spmv_plan_stats {
                                     bits 10 / 11: the pieces of a split sweep plan are cut with
                                     the even / the odd XCCs' units lighter (env
                                     SPMV_SWEEP_XCC_BIAS > 0 / < 0; the default cuts them evenly,
-                                    so a plan's layout depends only on the matrix and the chip) */
+                                    so a plan's layout depends only on the matrix and the chip);
+                                    bit 12: some 128-entry chunks span >= 65536 columns and keep
+                                    their absolute columns in the side table (kernel 2, delta
+                                    entries; variants reading 12-byte entries are refused) */
 } spmv_plan_stats;
 
 /* Build a plan from a device-resident CSR slice (row_ptr may start at any offset: entries are

@@ -1103,7 +1103,8 @@ int spmv_plan_get_stats(const spmv_plan *p, spmv_plan_stats *st)
                           (p->sweep_variant == 37 || p->sweep_variant == 38 || p->sweep_variant == 39) ? 128 : 0) |
                  (graph_form(p) == 2 ? 256 : graph_form(p) == 1 ? 512 : 0) |
                  (p->kernel == kKernelSweep && p->sweep_split > 1 && p->xbias_split > 0.0 ? 1024 : 0) |
-                 (p->kernel == kKernelSweep && p->sweep_split > 1 && p->xbias_split < 0.0 ? 2048 : 0);
+                 (p->kernel == kKernelSweep && p->sweep_split > 1 && p->xbias_split < 0.0 ? 2048 : 0) |
+                 (p->kernel == kKernelSweep && p->sweep_wide ? 4096 : 0);
     return 0;
 }
 

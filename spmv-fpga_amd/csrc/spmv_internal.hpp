@@ -171,6 +171,8 @@ struct spmv_plan {
     uint32_t *d_s_side = nullptr;    // absolute columns (lane order) of chunks with a gap > 511
     uint64_t sweep_side_chunks = 0;
     bool sweep_delta = false;
+    bool sweep_wide = false;         // some chunks span >= 65536 columns: their columns live only in
+                                     // the side table (delta plans; no 12-byte rc words can be rebuilt)
     // binned representation (kernel 6, binned.hip): reuses npanels, panel_rmax, d_panel_row and
     // ent_pad of the sweep fields; entries ordered (window, panel), segments padded
     uint32_t b_nwin = 0, b_W = 0;      // column windows of b_W columns (x staged in LDS by pass 1)

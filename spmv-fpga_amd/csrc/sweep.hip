@@ -907,7 +907,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_turn(
 // group c of G entries (a 128-entry chunk): base = min column; fails the plan's packing when the
 // span >= 65536
 __global__ void k_sweep_chunk_base(const uint32_t *__restrict__ col, uint64_t nchunks, uint32_t G,
-                                   uint32_t *__restrict__ cbase, uint32_t *__restrict__ bad)
+                                   uint32_t *__restrict__ cbase, uint32_t *__restrict__ bad, uint8_t *__restrict__ wide)
 {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchunks)
@@ -919,18 +919,33 @@ __global__ void k_sweep_chunk_base(const uint32_t *__restrict__ col, uint64_t nc
         hi = v > hi ? v : hi;
     }
     cbase[c] = lo;
+    wide[c] = hi - lo >= 65536u;
     if (hi - lo >= 65536u)
-        atomicOr(bad, 1u);
+        atomicAdd(bad, 1u);  // (the number of wide chunks)
 }
 
-// in place: col[k] <- (row << 16) | (col - base of k's group of 2^gshift entries)
+// in place: col[k] <- (row << 16) | (col - base of k's group of 2^gshift entries); a wide group
+// (its columns span >= 65536) keeps offset 0 here -- its absolute columns go to the side table
 __global__ void k_sweep_pack_rc(uint32_t *__restrict__ col, const uint16_t *__restrict__ row,
-                                const uint32_t *__restrict__ cbase, uint64_t n, uint32_t gshift)
+                                const uint32_t *__restrict__ cbase, uint64_t n, uint32_t gshift,
+                                const uint8_t *__restrict__ wide)
 {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n)
         return;
-    col[k] = ((uint32_t)row[k] << 16) | (col[k] - cbase[k >> gshift]);
+    const uint64_t c = k >> gshift;
+    col[k] = ((uint32_t)row[k] << 16) | (wide[c] ? 0u : col[k] - cbase[c]);
+}
+
+// the lane-order permutation of k_sweep_lane_order applied to one u32 array (a wide plan's
+// absolute columns, which follow their entries into the side table)
+__global__ void k_sweep_lane_order_u32(const uint32_t *__restrict__ in, uint64_t n, uint32_t *__restrict__ out)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    const uint64_t c = k & ~(uint64_t)127, w = k & 127;
+    out[c + 2 * (w & 63) + (w >> 6)] = in[k];
 }
 
 // Lane-order permutation inside each 128-entry chunk: memory word 2l+j holds logical entry
@@ -958,7 +973,8 @@ __global__ void k_sweep_lane_order(const uint32_t *__restrict__ rc_in, const V *
 // the row, in lane order; flag = some gap > 511 (the chunk's columns go to the side table).
 template <typename V>
 __global__ void k_sweep_delta(uint32_t *__restrict__ rc, V *__restrict__ val, uint64_t nchunks,
-                              uint16_t *__restrict__ row16, uint8_t *__restrict__ d8, uint8_t *__restrict__ flag)
+                              uint16_t *__restrict__ row16, uint8_t *__restrict__ d8, uint8_t *__restrict__ flag,
+                              const uint8_t *__restrict__ wide)
 {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchunks)
@@ -998,14 +1014,15 @@ __global__ void k_sweep_delta(uint32_t *__restrict__ rc, V *__restrict__ val, ui
         d8[c * G + m] = (uint8_t)d;
         prev = off;
     }
-    flag[c] = big ? 1 : 0;
+    flag[c] = big || wide[c] ? 1 : 0;  // (a wide chunk's offsets are all 0: the sort kept its order)
 }
 
 // per chunk: dbase = the chunk base, or bit 31 | its side-table index (sidx[c] != ~0), whose 128
 // absolute columns are written in lane order
 __global__ void k_sweep_delta_base(const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase,
                                    const uint32_t *__restrict__ sidx, uint64_t nchunks, uint32_t *__restrict__ dbase,
-                                   uint32_t *__restrict__ side)
+                                   uint32_t *__restrict__ side, const uint8_t *__restrict__ wide,
+                                   const uint32_t *__restrict__ abs_col)
 {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchunks)
@@ -1016,8 +1033,9 @@ __global__ void k_sweep_delta_base(const uint32_t *__restrict__ rc, const uint32
         return;
     }
     dbase[c] = 0x80000000u | k;
-    for (uint64_t m = 0; m < kSweepChunk; ++m)
-        side[(uint64_t)k * kSweepChunk + m] = cbase[c] + (rc[c * kSweepChunk + m] & 0xFFFFu);
+    for (uint64_t m = 0; m < kSweepChunk; ++m)  // (wide: the lane-ordered absolute columns)
+        side[(uint64_t)k * kSweepChunk + m] =
+            wide[c] ? abs_col[c * kSweepChunk + m] : cbase[c] + (rc[c * kSweepChunk + m] & 0xFFFFu);
 }
 
 // the 12-byte rc words of a delta plan, rebuilt from the delta arrays (one thread per chunk):
@@ -1050,6 +1068,10 @@ int sweep_materialize_rc(spmv_plan &p)
 {
     if (!p.sweep_delta || p.d_s_col || p.ent_pad == 0)
         return 0;
+    if (p.sweep_wide) {  // chunks spanning >= 65536 columns have no 16-bit offsets
+        set_error("sweep variant needs the 12-byte entries, which this plan's wide chunks cannot hold");
+        return 1;
+    }
     const uint64_t nchunks = p.ent_pad / kSweepChunk;
     SPMV_TRY(hipSetDevice(p.device));
     SPMV_TRY(hipMalloc((void **)&p.d_s_col, p.ent_pad * 4));
@@ -1569,9 +1591,11 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     uint32_t *k0 = nullptr, *k1 = nullptr, *i0 = nullptr, *i1 = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
+    uint8_t *d_wide = nullptr;     // per chunk: its columns span >= 65536 (side-table chunk)
+    uint32_t *d_abs = nullptr;     // a wide plan's absolute columns, lane-ordered
     auto cleanup = [&]() {
         for (void *q : {(void *)d_off, (void *)d_poff, (void *)d_rp, (void *)k0, (void *)k1, (void *)i0,
-                        (void *)i1, tmp})
+                        (void *)i1, tmp, (void *)d_wide, (void *)d_abs})
             if (q)
                 (void)hipFree(q);
     };
@@ -1621,25 +1645,47 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
         uint32_t *d_bad = d_off;  // reuse: d_off is no longer needed once the scatter ran
         SW_TRY(hipStreamSynchronize(s));
         SW_TRY(hipMemsetAsync(d_bad, 0, 4, s));
+        SW_TRY(hipMalloc((void **)&d_wide, std::max<uint64_t>(nchunks, 1)));
         if (nchunks)
             hipLaunchKernelGGL(k_sweep_chunk_base, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s,
-                               p.d_s_col, nchunks, group, p.d_s_cbase, d_bad);
+                               p.d_s_col, nchunks, group, p.d_s_cbase, d_bad, d_wide);
         SW_TRY(hipGetLastError());
         uint32_t bad = 0;
         SW_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
         SW_TRY(hipStreamSynchronize(s));
         const char *env = ablation_env("SPMV_SWEEP_PACKED");
         const bool want = !(env && env[0] == '0');
-        if (!bad && want && p.ent_pad) {
+        const char *lo = ablation_env("SPMV_SWEEP_LANE_ORDER");
+        const bool lane = !(lo && lo[0] == '0');
+        // the delta-coded entries below (SPMV_SWEEP_DELTA=0 keeps the 12-byte words only).
+        // SPMV_SWEEP_DETERMINISTIC=1 plans keep the 12-byte words: the turn kernel on the 11-byte
+        // entries measured 0.897 vs 0.871 ms (its deeper pipeline has no room for the decode,
+        // profiles/r03_delta_columns.jsonl r03p)
+        const char *de = std::getenv("SPMV_SWEEP_DELTA");
+        const bool delta = lane && !(de && de[0] == '0') && !det && nchunks && uint64_t(p.nr_cols) < (1ull << 31) &&
+                           rmax_used < 32768;
+        // a chunk whose columns span >= 65536 has no 16-bit offsets: the delta form carries its
+        // absolute columns in the side table (a plan with a few such chunks -- panels of a few
+        // entries spread over the columns, e.g. beside a long run of empty rows -- reads only the
+        // 11-byte entries). Side chunks stream 15 B per entry, so when more than 1 chunk in 10 is
+        // wide (sparse panels throughout), or without the delta form, the plan keeps the
+        // unpacked 14-byte entries
+        if ((!bad || (delta && uint64_t(bad) * 10 <= nchunks)) && want && p.ent_pad) {
+            if (bad) {
+                SW_TRY(hipMalloc((void **)&d_abs, p.ent_pad * 4));
+                hipLaunchKernelGGL(k_sweep_lane_order_u32, dim3((unsigned)((p.ent_pad + 255) / 256)), dim3(256), 0, s,
+                                   p.d_s_col, p.ent_pad, d_abs);
+                SW_TRY(hipGetLastError());
+                p.sweep_wide = true;
+            }
             hipLaunchKernelGGL(k_sweep_pack_rc, dim3((unsigned)((p.ent_pad + 255) / 256)), dim3(256), 0, s, p.d_s_col,
-                               p.d_s_row, p.d_s_cbase, p.ent_pad, gshift);
+                               p.d_s_row, p.d_s_cbase, p.ent_pad, gshift, d_wide);
             SW_TRY(hipGetLastError());
             SW_TRY(hipStreamSynchronize(s));
             SW_TRY(hipFree(p.d_s_row));
             p.d_s_row = nullptr;
             p.sweep_packed = true;
-            const char *lo = ablation_env("SPMV_SWEEP_LANE_ORDER");
-            if (!(lo && lo[0] == '0')) {
+            if (lane) {
                 uint32_t *rc2 = nullptr;
                 ValueType *v2 = nullptr;
                 SW_TRY(hipMalloc((void **)&rc2, p.ent_pad * 4));
@@ -1653,13 +1699,8 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                 p.d_s_col = rc2;
                 p.d_s_val = v2;
                 p.sweep_lane_order = true;
-                // delta-coded columns for the default kernel (env SPMV_SWEEP_DELTA=0 keeps the
-                // 12-byte words only). SPMV_SWEEP_DETERMINISTIC=1 plans keep the 12-byte words:
-                // the turn kernel on the 11-byte entries measured 0.897 vs 0.871 ms (its deeper
-                // pipeline has no room for the decode, profiles/r03_delta_columns.jsonl r03p)
-                const char *de = std::getenv("SPMV_SWEEP_DELTA");
-                if (!(de && de[0] == '0') && !det && nchunks && uint64_t(p.nr_cols) < (1ull << 31) &&
-                    rmax_used < 32768) {
+                // delta-coded columns for the default kernel (conditions above)
+                if (delta) {
                     uint8_t *d_flag = nullptr;
                     uint32_t *d_sidx = nullptr;
                     SW_TRY(hipMalloc((void **)&p.d_s_row16, p.ent_pad * 2));
@@ -1667,7 +1708,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                     SW_TRY(hipMalloc((void **)&p.d_s_dbase, nchunks * 4));
                     SW_TRY(hipMalloc((void **)&d_flag, nchunks));
                     hipLaunchKernelGGL((k_sweep_delta<ValueType>), dim3((unsigned)((nchunks + 63) / 64)), dim3(64), 0, s,
-                                       p.d_s_col, p.d_s_val, nchunks, p.d_s_row16, p.d_s_d8, d_flag);
+                                       p.d_s_col, p.d_s_val, nchunks, p.d_s_row16, p.d_s_d8, d_flag, d_wide);
                     hipError_t e = hipGetLastError();
                     std::vector<uint8_t> hf(nchunks);
                     if (e == hipSuccess)
@@ -1687,7 +1728,8 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
                     e = hipMemcpyAsync(d_sidx, sidx.data(), nchunks * 4, hipMemcpyHostToDevice, s);
                     if (e == hipSuccess) {
                         hipLaunchKernelGGL(k_sweep_delta_base, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s,
-                                           p.d_s_col, p.d_s_cbase, d_sidx, nchunks, p.d_s_dbase, p.d_s_side);
+                                           p.d_s_col, p.d_s_cbase, d_sidx, nchunks, p.d_s_dbase, p.d_s_side, d_wide,
+                                           d_abs);
                         e = hipGetLastError();
                     }
                     if (e == hipSuccess)

@@ -516,6 +516,36 @@ def test_sweep_variants_agree(torch, monkeypatch, packed, dtype):
     plan.destroy()
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sweep_wide_chunks_ride_in_the_side_table(torch, monkeypatch, dtype):
+    """A run of 60K empty rows leaves the panels beside it a few entries spread over the columns:
+    their 128-entry chunks span >= 65536 columns, which 16-bit offsets cannot hold. Those chunks
+    (well under 1 in 10) keep their absolute columns in the delta plan's side table (format bit
+    12) and the rest of the plan keeps the 11-byte entries. y is the oracle's; a variant that
+    needs the 12-byte entries is refused on such a plan."""
+    monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
+    rng = np.random.default_rng(33)
+    n = 3_000_000
+    lens = rng.poisson(16, n)
+    lens[100_000:160_000] = 0
+    lens[1_000_000:1_000_700] = 1  # and a stretch of single-entry rows
+    row_ptr = np.zeros(n + 1, np.int64)
+    row_ptr[1:] = np.cumsum(lens)
+    z = int(row_ptr[-1])
+    row_ptr = row_ptr.astype(np.uint32)
+    col = rng.integers(0, n, z, dtype=np.uint32)  # (unsorted within a row: CSR allows it)
+    val = rng.uniform(-1, 1, z).astype(dtype)
+    x = rng.uniform(0, 1, n).astype(dtype)
+    lib = spmv_hw.load(dtype)
+    y, st = run_device(torch, lib, row_ptr, col, val, x, n, expect_kernel="sweep")
+    assert st["format"] & 2 and st["format"] & 64 and st["format"] & 4096, st
+    check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y, dtype)
+    plan = spmv_hw.Plan.from_device(lib, to_dev(torch, row_ptr), to_dev(torch, col), to_dev(torch, val), n)
+    with pytest.raises(RuntimeError, match="wide chunks"):
+        plan.set_variant(94)
+    plan.destroy()
+
+
 def test_sweep_falls_back_to_unpacked_entries_on_sparse_panels(torch, monkeypatch):
     """A panel too sparse for 16-bit column offsets inside a 128-entry chunk (here 16K entries
     per panel over 10M columns: a chunk spans ~80K columns) keeps the 14-byte entries."""
