@@ -518,8 +518,8 @@ def test_sweep_variants_agree(torch, monkeypatch, packed, dtype):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_sweep_wide_chunks_ride_in_the_side_table(torch, monkeypatch, dtype):
-    """A run of 60K empty rows leaves the panels beside it a few entries spread over the columns:
-    their 128-entry chunks span >= 65536 columns, which 16-bit offsets cannot hold. Those chunks
+    """60K rows with an entry in every 50th only make panels of a few hundred entries spread over
+    the columns: their 128-entry chunks span >= 65536 columns, which 16-bit offsets cannot hold. Those chunks
     (well under 1 in 10) keep their absolute columns in the delta plan's side table (format bit
     12) and the rest of the plan keeps the 11-byte entries. y is the oracle's; a variant that
     needs the 12-byte entries is refused on such a plan."""
@@ -528,7 +528,7 @@ def test_sweep_wide_chunks_ride_in_the_side_table(torch, monkeypatch, dtype):
     n = 3_000_000
     lens = rng.poisson(16, n)
     lens[100_000:160_000] = 0
-    lens[1_000_000:1_000_700] = 1  # and a stretch of single-entry rows
+    lens[100_000:160_000:50] = 1  # one entry every 50th row: ~20K-row panels of ~400 entries
     row_ptr = np.zeros(n + 1, np.int64)
     row_ptr[1:] = np.cumsum(lens)
     z = int(row_ptr[-1])
