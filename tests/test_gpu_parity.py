@@ -518,17 +518,17 @@ def test_sweep_variants_agree(torch, monkeypatch, packed, dtype):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_sweep_wide_chunks_ride_in_the_side_table(torch, monkeypatch, dtype):
-    """60K rows with an entry in every 50th only make panels of a few hundred entries spread over
-    the columns: their 128-entry chunks span >= 65536 columns, which 16-bit offsets cannot hold. Those chunks
+    """A run of 49K empty rows at the top makes the first panels a few entries spread over the
+    columns: their 128-entry chunks span >= 65536 columns, which 16-bit offsets cannot hold. Those chunks
     (well under 1 in 10) keep their absolute columns in the delta plan's side table (format bit
     12) and the rest of the plan keeps the 11-byte entries. y is the oracle's; a variant that
     needs the 12-byte entries is refused on such a plan."""
     monkeypatch.setenv("SPMV_HW_KERNEL", "sweep")
-    rng = np.random.default_rng(33)
-    n = 3_000_000
+    rng = np.random.default_rng(21)
+    n = 6_000_000
     lens = rng.poisson(16, n)
-    lens[100_000:160_000] = 0
-    lens[100_000:160_000:50] = 1  # one entry every 50th row: ~20K-row panels of ~400 entries
+    lens[rng.random(n) < 0.2] = 0
+    lens[1000:50_000] = 0  # the first panels hold a few entries over ~20K rows each
     row_ptr = np.zeros(n + 1, np.int64)
     row_ptr[1:] = np.cumsum(lens)
     z = int(row_ptr[-1])
