@@ -607,7 +607,12 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
     // panels: y of <= rmax rows in LDS (fp64), plus the scratch slot of the pad entries
     const uint32_t rmax = (uint32_t)std::min<uint64_t>((kSweepLdsBytes - 256) / 8 - 1, 65534);
     std::vector<uint32_t> prow;
-    for (uint64_t P = std::max<uint64_t>({1, (n + rmax - 1) / rmax, std::min<uint64_t>(cus, n)});; ++P) {
+    // subdivide: as in build_sweep, a run of (nearly) empty rows longer than a panel that no
+    // nnz-balanced cut reaches ends a bounded search; the first P's cuts are then kept and any
+    // panel above rmax rows is split into panels of at most rmax rows
+    const uint64_t P_first = std::max<uint64_t>({1, (n + rmax - 1) / rmax, std::min<uint64_t>(cus, n)});
+    bool subdivide = false;
+    for (uint64_t P = P_first;; ++P) {
         if (P > (uint64_t)cus && P % cus)
             P = (P + cus - 1) / cus * cus;  // whole rounds of workgroups
         P = std::min<uint64_t>(P, std::max<uint64_t>(n, 1));
@@ -618,6 +623,9 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
             const uint64_t target = nnz * q / P;
             IndexType e = (q == P) ? n : (IndexType)(std::lower_bound(h_rp, h_rp + n + 1, (IndexType)target) - h_rp);
             e = std::max(e, r);
+            if (e - r > rmax && subdivide)
+                for (; e - r > rmax; r += rmax)
+                    prow.push_back(r + rmax);
             if (e - r > rmax)
                 ok = false;
             prow.push_back(e);
@@ -625,9 +633,13 @@ int build_binned(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src
         }
         if (ok)
             break;
-        if (P >= n) {
-            set_error("build_binned: cannot form panels");
-            return 1;
+        if (P >= n || P > 8 * std::max<uint64_t>(P_first, (uint64_t)cus)) {
+            if (subdivide) {
+                set_error("build_binned: cannot form panels");
+                return 1;
+            }
+            subdivide = true;
+            P = P_first - 1;  // (++P)
         }
     }
     const uint32_t P = (uint32_t)(prow.size() - 1);

@@ -1448,7 +1448,13 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     if (!(xbias > -0.5 && xbias < 0.5))
         xbias = xbias_split = 0.0;
     std::vector<uint32_t> prow;
-    for (uint64_t P = std::max<uint64_t>(1, (n + rmax - 1) / rmax);; ++P) {
+    // subdivide: a run of (nearly) empty rows longer than a panel that no nnz-balanced cut reaches
+    // -- most often trailing empty rows -- made every P fail (and the search ran on to P = n);
+    // after a bounded search the cuts are taken at the first P and any panel above the LDS rows is
+    // split into panels of at most rmax rows
+    const uint64_t P_first = std::max<uint64_t>(1, (n + rmax - 1) / rmax);
+    bool subdivide = false;
+    for (uint64_t P = P_first;; ++P) {
         {
             // pieces pay when the slice fills at most half the workgroups with full panels and
             // the partial sums (split * n fp64 values, written once and read once by the
@@ -1456,7 +1462,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             // power-law matrix 14 % faster (partials 0.42x the entries), the N = 8 slice of
             // the 10M/160M matrix 18 % (0.33x), a 300K-row matrix 25 % slower (1.4x)
             const uint64_t S = P ? (uint64_t)cus / P : 0;
-            split_mode = allow_split && S >= 2 && P * S * 10 >= (uint64_t)cus * 9 &&
+            split_mode = !subdivide && allow_split && S >= 2 && P * S * 10 >= (uint64_t)cus * 9 &&
                          (force_split || 2 * S * n * acc * 5 <= 3 * nnz * (4 + sizeof(ValueType)));
         }
         if (!split_mode && P > 1 && P % cus)
@@ -1474,6 +1480,9 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             e = std::max(e, r);
             if (e - r > rmax && xbias != 0.0 && !split_mode && q < P)
                 e = r + rmax;  // a biased cut past the LDS rows: this panel takes what fits
+            if (e - r > rmax && subdivide)
+                for (; e - r > rmax; r += rmax)
+                    prow.push_back(r + rmax);
             if (e - r > rmax)
                 ok = false;
             prow.push_back(e);
@@ -1486,9 +1495,14 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             --P;
             continue;
         }
-        if (P >= n) {
-            set_error("build_sweep: cannot form panels");
-            return 1;
+        if (P >= n || P > 8 * std::max<uint64_t>(P_first, (uint64_t)cus)) {
+            if (subdivide) {
+                set_error("build_sweep: cannot form panels");
+                return 1;
+            }
+            subdivide = true;
+            xbias = 0.0;
+            P = P_first - 1;  // (++P)
         }
     }
     const uint32_t P = (uint32_t)(prow.size() - 1);

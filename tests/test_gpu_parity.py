@@ -1471,3 +1471,43 @@ def test_sweep_work_stealing_forced_splits(torch, monkeypatch, name, pieces):
         check(row_ptr, col, val, x, y_gold, y.cpu().numpy()[:n], np.float64)
     plan.destroy()
     assert st["kernel"] == 2
+
+
+def _empty_run_csr(rng, n, run, dtype):
+    """Poisson(16) rows with a run of empty rows at `run` (slice), random columns."""
+    lens = rng.poisson(16, n)
+    lens[run] = 0
+    row_ptr = np.zeros(n + 1, np.int64)
+    row_ptr[1:] = np.cumsum(lens)
+    z = int(row_ptr[-1])
+    col = rng.integers(0, n, z, dtype=np.uint32)
+    val = rng.uniform(-1, 1, z).astype(dtype)
+    x = rng.uniform(0, 1, n).astype(dtype)
+    return row_ptr.astype(np.uint32), col, val, x
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("case", ["trailing_fp64_sweep", "trailing_fp64_nobias", "middle_fp64_nobias",
+                                  "trailing_fp32_binned"])
+def test_panels_past_a_long_run_of_empty_rows(torch, monkeypatch, case):
+    """A run of empty rows longer than a panel (here the last 30K rows of 1M, or 60K in the
+    middle) that no nnz-balanced cut can reach: the panel search is bounded and the panel over
+    the run is split into panels of at most the LDS rows -- the plan builds in seconds (it used
+    to search on to P = n and fail) and y is the oracle's. For the sweep (fp64) and the binned
+    kernel (fp32, >= 5M columns), with and without the XCC bias (whose clipped cuts covered a
+    middle run but not a trailing one)."""
+    import time
+    dtype = np.float32 if "fp32" in case else np.float64
+    n = 6_000_000 if "fp32" in case else 1_000_000
+    run = slice(100_000, 160_000) if case.startswith("middle") else slice(n - 30_000 if n < 5_000_000 else n - 100_000, n)
+    if "nobias" in case:
+        monkeypatch.setenv("SPMV_SWEEP_XCC_BIAS", "0")
+    rng = np.random.default_rng(5)
+    row_ptr, col, val, x = _empty_run_csr(rng, n, run, dtype)
+    lib = spmv_hw.load(dtype)
+    t0 = time.perf_counter()
+    y, st = run_device(torch, lib, row_ptr, col, val, x, n)
+    assert time.perf_counter() - t0 < 60
+    assert st["kernel"] == (6 if "binned" in case else 2), st
+    check(row_ptr, col, val, x, oracle.spmv_gold(row_ptr, col, val, x), y, dtype)
+    assert not np.any(y[run])
