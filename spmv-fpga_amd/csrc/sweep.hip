@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <tuple>
 #include <cmath>
 #include <cstring>
 
@@ -442,8 +443,16 @@ __device__ void combine_behind(const uint32_t *__restrict__ panel_row, const uin
     }
 }
 
+// The packed sweep. FL... is empty for every launch but one: spmv_hw's streamed copy-back
+// launches it with (uint32_t *yflag, uint32_t yepoch, V *yhost) -- each panel flagged in host
+// memory once its y is stored (and, in the tools build's direct form, stored into host memory).
+// With FL empty the kernel is the plain sweep, instruction for instruction the kernel before the
+// flags existed (same registers, same 176-byte argument block) and as fast (418.6-420.3 vs
+// 418.8-420.1 GFLOP/s, interleaved on one box); one kernel taking the extra arguments measured
+// 1.3 % slower on the headline matrix, and so did a body shared by two entry points through a
+// force-inlined function (profiles/r06u_flag_kernel_ab.txt).
 template <typename V, int T, int Q, bool NT, int LAG = 0, int ABL = 0, typename A = double, bool DL = false,
-          bool ST = false>
+          bool ST = false, typename... FL>
 __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     const uint32_t *__restrict__ rc, const uint32_t *__restrict__ cbase, const V *__restrict__ val,
     const uint32_t *__restrict__ panel_row, const uint32_t *__restrict__ unit_ent,
@@ -452,8 +461,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     V *__restrict__ y, const uint16_t *__restrict__ row16, const uint8_t *__restrict__ d8,
     const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ side, unsigned long long *__restrict__ steal,
     uint32_t tail16, uint32_t nunits, const A *__restrict__ cpart, uint32_t *__restrict__ ccount,
-    uint32_t *__restrict__ cnext, uint32_t npanels, uint32_t cj, uint32_t *__restrict__ yflag, uint32_t yepoch,
-    V *__restrict__ yhost)
+    uint32_t *__restrict__ cnext, uint32_t npanels, uint32_t cj, FL... fl)
 {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -707,15 +715,21 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
         lds_add(&ylds[R], sink);
     __syncthreads();
     ABL_WG_STAMP(1);
-    // (yhost: the tools build's direct form of spmv_hw's copy-back -- the panel's y stored straight
-    // into pinned host memory over PCIe instead of device memory; plans of one piece per panel)
-    write_panel<V, T, A>(ylds, R, (yhost ? yhost : y) + r0, pieces, part, stride, panel_unit[p],
-                         pcnt ? pcnt + p : nullptr);
-    if (yflag) {
-        // spmv_hw's streamed copy-back (plans of one piece per panel only): the panel's y is
-        // published at system scope -- every wave's stores complete, one lane's release writes
-        // the XCD L2's dirty lines back to memory -- and its flag in host memory is set to this
-        // call's epoch; the host then copies the panel's rows while the other panels still sweep
+    if constexpr (sizeof...(FL) == 0) {
+        write_panel<V, T, A>(ylds, R, y + r0, pieces, part, stride, panel_unit[p], pcnt ? pcnt + p : nullptr);
+    } else {
+        // spmv_hw's streamed copy-back (plans of one piece per panel only). yhost: the tools
+        // build's direct form -- the panel's y stored straight into pinned host memory over PCIe
+        // instead of device memory. Then the panel's y is published at system scope -- every
+        // wave's stores complete, one lane's release writes the XCD L2's dirty lines back to
+        // memory -- and its flag in host memory is set to this call's epoch; the host copies the
+        // panel's rows while the other panels still sweep
+        const auto args = std::make_tuple(fl...);
+        uint32_t *yflag = std::get<0>(args);
+        const uint32_t yepoch = std::get<1>(args);
+        V *yhost = std::get<2>(args);
+        write_panel<V, T, A>(ylds, R, (yhost ? yhost : y) + r0, pieces, part, stride, panel_unit[p],
+                             pcnt ? pcnt + p : nullptr);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0)
@@ -723,6 +737,7 @@ __global__ __launch_bounds__(T) void k_spmv_sweep_packed(
     }
     ABL_WG_STAMP(2);
 }
+
 
 // Deterministic form (env SPMV_SWEEP_DETERMINISTIC=1): the same plan, layout and gathers as
 // k_spmv_sweep_packed / k_spmv_sweep, but the LDS adds of a workgroup are ordered. In the default
@@ -1230,15 +1245,27 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, Q, NT, LAG, ABL, A>, grid, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        (const uint16_t *)nullptr, (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr, \
-                       (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, 0u, \
-                       p.y_flag, p.y_epoch, p.y_host)
+                       (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, 0u)
     // the default kernel on delta-coded columns (variant 28's loose sync: 2 groups, lag 2)
 #define PKD(ST, TAIL)                                                                                 \
     launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, ST>, gridb, block, lds, s, p.d_s_col, \
                        p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, p.panel_rmax + 1, pcnt, d_x, d_y, \
                        p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side, ST ? p.d_steal : (unsigned long long *)nullptr, (uint32_t)(TAIL), \
-                       (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels, bh.rows_per_thread, \
-                       p.y_flag, p.y_epoch, p.y_host)
+                       (uint32_t)p.nunits, reinterpret_cast<const A *>(bh.cpart), bh.ccount, bh.cnext, (uint32_t)p.npanels, bh.rows_per_thread)
+    // spmv_hw's streamed copy-back (p.y_flag set: plans of one piece per panel, default variant)
+#define PKDF()                                                                                        \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, true, false, uint32_t *, uint32_t, ValueType *>, gridb, block, lds, s, \
+                   p.d_s_col, p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part, \
+                   p.panel_rmax + 1, pcnt, d_x, d_y, p.d_s_row16, p.d_s_d8, p.d_s_dbase, p.d_s_side,               \
+                   (unsigned long long *)nullptr, 0u, (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr,  \
+                   (uint32_t *)nullptr, (uint32_t)p.npanels, 0u, p.y_flag, p.y_epoch, p.y_host)
+#define PKF()                                                                                         \
+    launch_or_warm(warm, k_spmv_sweep_packed<ValueType, T, 2, true, 2, 0, A, false, false, uint32_t *, uint32_t, ValueType *>, grid, block, lds, s, p.d_s_col, \
+                   p.d_s_cbase, p.d_s_val, p.d_panel_row, p.d_unit_ent, p.d_unit_panel, p.d_panel_unit, part,        \
+                   p.panel_rmax + 1, pcnt, d_x, d_y, (const uint16_t *)nullptr, (const uint8_t *)nullptr,           \
+                   (const uint32_t *)nullptr, (const uint32_t *)nullptr, (unsigned long long *)nullptr, 0u,          \
+                   (uint32_t)p.nunits, (const A *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, 0u,        \
+                   p.y_flag, p.y_epoch, p.y_host)
 #define PK(Q, LAG) PKN(true, Q, LAG, 0)
 #define PKA(ABL) PKN(true, 2, 2, ABL)
         switch (p.sweep_variant) {
@@ -1284,13 +1311,17 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
                     break;
                 }
 #endif
-                PKD(false, 0);
+                if (p.y_flag || warm) PKDF();  // (warm: load the flagged code object too)
+                if (!p.y_flag) PKD(false, 0);
             } else {
-                PK(2, 2);
+                if (p.y_flag || warm) PKF();
+                if (!p.y_flag) PK(2, 2);
             }
             break;
         }
 #undef PKD
+#undef PKDF
+#undef PKF
 #undef PKA
 #undef PK
 #undef PKN
