@@ -110,6 +110,8 @@ def test_bench_one_rank_rccl_rehearsal(scaling):
         # the north star's literal mapping at world 1: spmv_hw with one unit, RCCL reduce merge
         di = d["dropin"]
         assert di["pass"] and di["units"] == 1 and di["merge"] == "reduce", di
+        hm = di["host_merge"]  # then the library's default merge (each GPU's slice over PCIe)
+        assert hm["pass"] and hm["merge"] == "host" and hm["units"] == 1 and hm["verification"] == [0] * hm["calls"], hm
         e2e = d["value_e2e_form"]
         assert d["value_e2e"] < d["value"] and e2e["exchange_ms"] == nat["reduce_exchange_ms"], e2e
         assert all(nat[k] > 0 for k in ("gather_compute_ms", "reduce_exchange_ms", "allgather_graph_ms_per_step"))
