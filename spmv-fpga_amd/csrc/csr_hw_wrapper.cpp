@@ -229,6 +229,32 @@ int env_pieces(int dflt)
     return e ? std::max(1, std::atoi(e)) : dflt;
 }
 
+// Panel bounds of a streamed copy-back's k pieces over P panels. The copy engine runs the pieces
+// back to back, so what is left when the last copy lands is that piece's host add: the pieces
+// taper (weights 16, 16, ..., 8, 4, 2, 1, 1 -- the last two 1/64 of y each at k = 8) instead of
+// k equal parts. The tools build's SPMV_HW_PIECE_SHAPE=equal gives the equal parts.
+std::vector<uint32_t> piece_bounds(uint32_t P, uint32_t k)
+{
+    std::vector<uint32_t> q(k + 1, 0);
+    const char *sh = ablation_env("SPMV_HW_PIECE_SHAPE");
+    const bool equal = k < 4 || (sh && std::strcmp(sh, "equal") == 0);
+    std::vector<uint64_t> w(k, 1);
+    if (!equal)
+        for (int j = (int)k - 3; j >= 0; --j)
+            w[j] = std::min<uint64_t>(16, 2 * w[j + 1]);
+    uint64_t W = 0;
+    for (uint64_t v : w)
+        W += v;
+    uint64_t c = 0;
+    for (uint32_t j = 1; j <= k; ++j) {
+        c += w[j - 1];
+        // at least one panel per piece (k <= P)
+        const uint64_t b = uint64_t(P) * c / W;
+        q[j] = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(b, q[j - 1] + 1), P - (k - j));
+    }
+    return q;
+}
+
 // Copies rows [0, rows) of a device y slice into pinned staging on stream s as `pieces` copies,
 // each followed by an event, and appends one add_part per piece (dst = the caller's y). The
 // host adds of a piece then start while later pieces are still crossing PCIe. 8 pieces of y in
@@ -275,6 +301,8 @@ struct streamed_piece {
     std::atomic<int> state{0};
     std::string err;
     double t_ready = 0.0, t_enq = 0.0;  // (SPMV_HW_TRACE) flags all seen / copy enqueued, timestamp_us
+    std::atomic<int64_t> t_landed{0};   // (SPMV_HW_TRACE) first adding thread to see the copy done, us
+    hipEvent_t t_copied = nullptr;      // (SPMV_HW_TRACE) timing event after the copy, device clock
     bool by_flags = false;              // the flags, not the end of the kernels, released the piece
 };
 
@@ -288,7 +316,11 @@ int wait_streamed(void *ready, std::string *err)
         *err = pc->err;
         return 1;
     }
-    return pc->ev ? wait_event(pc->ev, err) : 0;  // (direct form: the flags were the landing)
+    if (pc->ev && wait_event(pc->ev, err))
+        return 1;  // (direct form: the flags were the landing)
+    int64_t none = 0;
+    pc->t_landed.compare_exchange_strong(none, (int64_t)timestamp_us(), std::memory_order_relaxed);
+    return 0;
 }
 
 // Copy each piece as soon as its panels are flagged, in landing order, on the calling thread --
@@ -359,6 +391,8 @@ double feed_pieces(std::vector<streamed_piece> &pcs, const std::vector<hw_matrix
                                    hipMemcpyDeviceToHost, m->copy_stream);
             if (e == hipSuccess)
                 e = hipEventRecord(pc.ev, m->copy_stream);
+            if (e == hipSuccess && pc.t_copied)
+                e = hipEventRecord(pc.t_copied, m->copy_stream);
             if (e != hipSuccess)
                 fail = std::string("y copy: ") + hipGetErrorString(e);
             pc.t_enq = timestamp_us();
@@ -381,9 +415,11 @@ double feed_pieces(std::vector<streamed_piece> &pcs, const std::vector<hw_matrix
 // to 16 host threads; returns when (timestamp_us) the last copy was seen complete. The
 // documented knob SPMV_HW_PREFAULT=0 lets the adds take the page faults; the split and thread
 // count are switches of the tools build.
-double accumulate(const std::vector<add_part> &parts, int (*wait)(void *, std::string *) = wait_event)
+double accumulate(const std::vector<add_part> &parts, int (*wait)(void *, std::string *) = wait_event,
+                  int threads = accum_options().threads)
 {
     accum_options o;
+    o.threads = threads;
     const char *pf = std::getenv("SPMV_HW_PREFAULT");
     o.prefault = !(pf && pf[0] == '0');
     const char *se = ablation_env("SPMV_HW_ADD_SPLIT");
@@ -425,19 +461,22 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
         n += k;
     }
     std::vector<streamed_piece> pcs(n);
+    std::vector<std::vector<uint32_t>> qb;
+    for (auto &c : cuts)
+        qb.push_back(piece_bounds((uint32_t)c.first->panel_rows.size() - 1, c.second));
     size_t i = 0;
     for (uint32_t j = 0, more = 1; more; ++j) {
         more = 0;
-        for (auto &c : cuts) {
+        for (size_t ci = 0; ci < cuts.size(); ++ci) {
+            auto &c = cuts[ci];
             if (j >= c.second)
                 continue;
             more = 1;
             hw_matrix_impl *m = c.first;
-            const uint32_t P = (uint32_t)m->panel_rows.size() - 1;
             streamed_piece &pc = pcs[i++];
             pc.m = m;
-            pc.q0 = (uint32_t)(uint64_t(P) * j / c.second);
-            pc.q1 = (uint32_t)(uint64_t(P) * (j + 1) / c.second);
+            pc.q0 = qb[ci][j];
+            pc.q1 = qb[ci][j + 1];
             pc.b = m->panel_rows[pc.q0];
             pc.e = m->panel_rows[pc.q1];
             m->done.device = m->device;
@@ -455,11 +494,25 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
                     (direct ? pcs[k].m->h_direct : pcs[k].m->h_stage) + pcs[k].b, pcs[k].e - pcs[k].b,
                     static_cast<void *>(&pcs[k])};
 
+    // (SPMV_HW_TRACE) device-clock times of each piece's copy, from its unit's kernel launch
+    std::vector<hipEvent_t> t_launch(units, nullptr);
+    if (trace) {
+        for (int u = 0; u < units; ++u) {
+            check(hipSetDevice(impl(hw_matrix[u])->device), "hipSetDevice");
+            check(hipEventCreate(&t_launch[u]), "hipEventCreate");
+        }
+        for (streamed_piece &pc : pcs) {
+            check(hipSetDevice(pc.m->device), "hipSetDevice");
+            check(hipEventCreate(&pc.t_copied), "hipEventCreate");
+        }
+    }
     const double hw_s = timestamp_us();
     for (int u = 0; u < units; ++u) {
         hw_matrix_impl *m = impl(hw_matrix[u]);
         if (m->row_end == m->row_begin)
             continue;
+        if (t_launch[u])
+            check(hipEventRecord(t_launch[u], unit_stream(u)), "hipEventRecord");
         if (++m->epoch == 0)  // (0 is the flags' initial value)
             m->epoch = 1;
         m->plan->y_flag = m->d_flags;
@@ -476,7 +529,11 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
     for (auto &c : cuts)
         us.push_back(c.first);
     double landed = 0.0;
-    std::thread adder([&] { landed = accumulate(parts, wait_streamed); });
+    // 8 adding threads: the streamed adds keep pace with the copy engine's ~52 GB/s on 8, and
+    // fewer threads leave the feeding thread its core (interleaved A/B on the 10M/160M plan,
+    // profiles/r06zg_spmv_hw_pieces_threads_ab.jsonl: Total 2.09 / 2.15 / 2.20 ms on 8 / 12 / 16
+    // threads; the unstreamed merge, whose adds start after the kernel, keeps 16)
+    std::thread adder([&] { landed = accumulate(parts, wait_streamed, 8); });
     const double hw_f = us.empty() ? timestamp_us() : feed_pieces(pcs, us, trace ? &seen : nullptr);
     for (hw_matrix_impl *m : us)
         m->plan->y_host = nullptr;
@@ -494,11 +551,28 @@ void spmv_hw_streamed(csr_hw_matrix **hw_matrix, int units, hw_vector_impl *x, c
             std::fprintf(stderr, "spmv_hw trace:   unit 0: %zu of %zu panel flags seen while the pieces were fed; "
                                  "first %.3f, median %.3f, last %.3f ms after the launch\n",
                          t.size(), seen.size(), t.front(), t[t.size() / 2], t.back());
-        for (const streamed_piece &pc : pcs)  // when each piece was released and its copy enqueued, from the launch
-            std::fprintf(stderr, "spmv_hw trace:   piece unit %d panels [%u, %u) ready %.3f ms (%s), enqueued %.3f ms\n",
+        for (const streamed_piece &pc : pcs) {
+            // when each piece was released, its copy enqueued, the copy done (device clock, from
+            // the unit's kernel launch) and first seen done by an adding thread (host clock)
+            float copied = -1.0f;  // (the direct form records no copy; a failed query would stay
+                                   // behind as the thread's last error for the next launch check)
+            if (pc.ev && pc.t_copied && hipEventElapsedTime(&copied, t_launch[pc.m->unit], pc.t_copied) != hipSuccess) {
+                copied = -1.0f;
+                (void)hipGetLastError();
+            }
+            std::fprintf(stderr,
+                         "spmv_hw trace:   piece unit %d panels [%u, %u) ready %.3f ms (%s), enqueued %.3f ms, "
+                         "copied %.3f ms (device), landed %.3f ms\n",
                          pc.m->unit, pc.q0, pc.q1, (pc.t_ready - hw_s) / 1000, pc.by_flags ? "flags" : "kernel end",
-                         (pc.t_enq - hw_s) / 1000);
+                         (pc.t_enq - hw_s) / 1000, copied, (double(pc.t_landed.load()) - hw_s) / 1000);
+        }
     }
+    for (streamed_piece &pc : pcs)
+        if (pc.t_copied)
+            (void)hipEventDestroy(pc.t_copied);
+    for (hipEvent_t e : t_launch)
+        if (e)
+            (void)hipEventDestroy(e);
     tr("spmv_hw: accumulation after the kernels", hw_f);
     const double ra_exec = std::max(0.0, (timestamp_us() - hw_f) / 1000.0);
     std::printf("Result accumulation time : %.6f ms elapsed\n", ra_exec);

@@ -42,6 +42,24 @@ def _flow(lib, h_rp, h_col, h_val, h_x, calls):
     return ys
 
 
+def _check_tapered_pieces(err, units, calls):
+    """The trace's pieces (csr_hw_wrapper.cpp piece_bounds): per call and unit, whole panels
+    that tile [0, P) in order, 8 / units of them (at least 2), tapering -- no piece larger than
+    the one before it -- so the last copy to land leaves a small add (the last is 1/16 of the
+    first at 8 pieces, 1/4 at 4)."""
+    found = [(int(u), int(a), int(b)) for u, a, b in re.findall(r"piece unit (\d+) panels \[(\d+), (\d+)\)", err)]
+    assert len(found) % calls == 0 and found, err[-2000:]
+    per_call = found[:len(found) // calls]
+    k = max(2, 8 // units)
+    for u in range(units):
+        ps = [(a, b) for v, a, b in per_call if v == u]
+        assert len(ps) == k and ps[0][0] == 0, ps
+        assert all(ps[j][1] == ps[j + 1][0] for j in range(k - 1)), ps
+        sizes = [b - a for a, b in ps]
+        assert all(sizes[j] + 1 >= sizes[j + 1] >= 1 for j in range(k - 1)), sizes  # (+1: rounding)
+        assert sizes[-1] * (16 if k >= 8 else 4) <= sizes[0] + 16, sizes  # (weights 16..1, 1 / 4, 2, 1, 1)
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("units", [1, 2])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
@@ -61,6 +79,7 @@ def test_streamed_copy_back_matches_the_oracle(monkeypatch, capfd, units, dtype)
     ys = _flow(lib, *h, calls=3)
     _, err = capfd.readouterr()
     assert err.count("D2H landed (streamed)") == 3, err[-2000:]
+    _check_tapered_pieces(err, units, calls=3)
     ref = oracle.spmv_gold(*h) if dtype == np.float64 else oracle.spmv_fp64acc(*h)
     tight = 1e-12 if dtype == np.float64 else 2e-6
     assert oracle.scaled_error(*h, ref, ys[0]) <= tight
@@ -90,6 +109,7 @@ def test_streamed_copy_back_at_headline_size(monkeypatch, capfd):
     ys = _flow(lib, *h, calls=3)
     out, err = capfd.readouterr()
     assert err.count("D2H landed (streamed)") == 3
+    _check_tapered_pieces(err, 1, calls=3)
     ref = oracle.spmv_gold(*h)
     assert oracle.scaled_error(*h, ref, ys[0]) <= 1e-12
     assert lib.verification(ref, ys[0]) == 0

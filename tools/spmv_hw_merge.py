@@ -31,7 +31,8 @@ import torch  # noqa: E402
 import spmv_hw  # noqa: E402
 
 KNOBS = {"pipe": "SPMV_HW_PIPELINE", "pieces": "SPMV_HW_PIECES", "split": "SPMV_HW_ADD_SPLIT",
-         "threads": "SPMV_HW_ADD_THREADS", "stream": "SPMV_HW_STREAM", "direct": "SPMV_HW_DIRECT"}
+         "threads": "SPMV_HW_ADD_THREADS", "stream": "SPMV_HW_STREAM", "direct": "SPMV_HW_DIRECT",
+         "shape": "SPMV_HW_PIECE_SHAPE"}
 LINES = {"hw_ms": "Hardware execution time", "accum_ms": "Result accumulation time", "total_ms": "Total time"}
 
 
@@ -89,11 +90,13 @@ def main():
     ap.add_argument("--merges", default="host,gather,reduce")
     ap.add_argument("--variants", default="default;pipe=0",
                     help="';'-separated knob sets, e.g. 'default;pipe=0;pieces=8,split=0' (knobs: %s)" % ", ".join(KNOBS))
+    ap.add_argument("--tools", action="store_true",
+                    help="load the tools build (lib/ablations), where the pieces / split / threads knobs apply")
     a = ap.parse_args()
     dtype = np.float64 if a.dtype == "f64" else np.float32
     ndev = torch.cuda.device_count()
     os.environ["SPMV_NGPUS"] = str(ndev)
-    lib = spmv_hw.load(dtype)
+    lib = spmv_hw.load(dtype, ablations=a.tools)
     n = a.rows
     rp, col, val, _ = spmv_hw.gen_powerlaw(lib, n, n, a.nnz, seed=4)
     x = spmv_hw.gen_vector(lib, n, seed=6)
