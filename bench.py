@@ -621,7 +621,7 @@ def run_dropin(args, units, merge, ref, sw_ms, timeout):
            "total_gflops_median": round(2.0 * d["nnz"] / (med(tot) * 1e-3) / 1e9, 3) if med(tot) > 0 else None,
            "software_execution_ms": round(sw_ms, 3) if sw_ms else None,
            # the same matrix's calls with SPMV_HW_STREAM=0 (y copied back after the kernel; the
-           # streamed copy-back applies to one-piece-per-panel sweep plans with the host merge)
+           # streamed copy-back applies to one-piece-per-panel sweep and binned plans with the host merge)
            "unstreamed_total_ms": {"median": med(ab_tot), "calls": ab_tot} if ab_tot else None,
            "verification": [c["verification"] for c in calls],
            "max_rel_diff_vs_spmv_gold": max(c["max_rel_diff"] for c in calls), "tol": tol,

@@ -48,6 +48,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <tuple>
 #include <vector>
 
 #include "spmv_internal.hpp"
@@ -224,11 +225,15 @@ __global__ __launch_bounds__(kBinT) void k_bin_mul(const V *__restrict__ x, uint
 // ABL (measurement-only ablations, tools library; wrong y): 1 = no LDS adds (products summed into
 // a register, added once at the end: the memory stream alone), 2 = loads re-read the wave's first
 // 16 steps (L2-resident: the LDS adds and decode alone)
-template <typename V, bool DELTA, int ABL = 0>
+// FL...: empty, or (uint32_t *yflag, uint32_t yepoch) for spmv_hw's streamed copy-back -- each
+// panel's flag in host memory set to the call's epoch once its rows of y are published (the
+// sweep's scheme, sweep.hip k_spmv_sweep_packed); the plain instantiation is untouched by it.
+template <typename V, bool DELTA, int ABL = 0, typename... FL>
 __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, const void *__restrict__ rowp,
                                                    const uint64_t *__restrict__ seg,
                                                    const uint32_t *__restrict__ panel_row, uint32_t nwin,
-                                                   uint32_t npan, uint32_t slots, V *__restrict__ y, uint64_t mirror)
+                                                   uint32_t npan, uint32_t slots, V *__restrict__ y, uint64_t mirror,
+                                                   FL... fl)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double *ys = reinterpret_cast<double *>(smem);
@@ -353,6 +358,15 @@ __global__ __launch_bounds__(kBinT) void k_bin_acc(const V *__restrict__ prod, c
     const uint32_t r0 = panel_row[p], nr = panel_row[p + 1] - r0;
     for (uint32_t i = threadIdx.x; i < nr; i += kBinT)
         y[r0 + i] = (V)ys[i];
+    if constexpr (sizeof...(FL) != 0) {
+        // every wave's stores complete, then one lane's system-scope release publishes the
+        // panel's rows and sets its flag
+        const auto args = std::make_tuple(fl...);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(std::get<0>(args) + p, std::get<1>(args), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     BN_STAMP(1, 1);
 }
 
@@ -547,12 +561,25 @@ hipError_t launch_binned(const spmv_plan &p, const ValueType *d_x, ValueType *d_
         return hipGetLastError();
     }
 #endif
-    if (p.b_delta)
-        launch_or_warm(warm, k_bin_acc<ValueType, true>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod, rowp,
-                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
-    else
-        launch_or_warm(warm, k_bin_acc<ValueType, false>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod, rowp,
-                       seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
+    // spmv_hw's streamed copy-back: the flagged pass 2 (sweep_can_flag_panels)
+    if (p.y_flag || warm) {
+        if (p.b_delta)
+            launch_or_warm(warm, k_bin_acc<ValueType, true, 0, uint32_t *, uint32_t>, dim3((unsigned)p.npanels),
+                           dim3(kBinT), lds2, s, prod, rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels,
+                           p.panel_rmax + 1, d_y, mirror2, p.y_flag, p.y_epoch);
+        else
+            launch_or_warm(warm, k_bin_acc<ValueType, false, 0, uint32_t *, uint32_t>, dim3((unsigned)p.npanels),
+                           dim3(kBinT), lds2, s, prod, rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels,
+                           p.panel_rmax + 1, d_y, mirror2, p.y_flag, p.y_epoch);
+    }
+    if (!p.y_flag) {
+        if (p.b_delta)
+            launch_or_warm(warm, k_bin_acc<ValueType, true>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod,
+                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
+        else
+            launch_or_warm(warm, k_bin_acc<ValueType, false>, dim3((unsigned)p.npanels), dim3(kBinT), lds2, s, prod,
+                           rowp, seg, p.d_panel_row, p.b_nwin, (uint32_t)p.npanels, p.panel_rmax + 1, d_y, mirror2);
+    }
     return hipGetLastError();
 }
 

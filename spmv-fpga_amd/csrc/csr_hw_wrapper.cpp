@@ -213,7 +213,8 @@ void setup_streaming(hw_matrix_impl *m)
     check(hipHostGetDevicePointer((void **)&m->d_flags, m->h_flags, 0), "hipHostGetDevicePointer(panel flags)");
     check(hipStreamCreateWithFlags(&m->copy_stream, hipStreamNonBlocking), "hipStreamCreate");
     const uint64_t rows = m->row_end - m->row_begin;
-    if (ablation_env("SPMV_HW_DIRECT")) {  // the measurement form: y straight into host memory
+    if (ablation_env("SPMV_HW_DIRECT") && pl.kernel == kKernelSweep) {  // the measurement form: y straight
+                                                                         // into host memory (sweep only)
         check(hipHostMalloc((void **)&m->h_direct, rows * sizeof(ValueType), hipHostMallocCoherent | hipHostMallocMapped),
               "hipHostMalloc(direct y)");
         check(hipHostGetDevicePointer((void **)&m->d_direct, m->h_direct, 0), "hipHostGetDevicePointer(direct y)");

@@ -1345,6 +1345,8 @@ static void launch_sweep_t(const spmv_plan &p, const ValueType *d_x, ValueType *
 // with the combine kernel: those whose launch can carry the previous step's combine
 bool sweep_can_flag_panels(const spmv_plan &p)
 {
+    if (p.kernel == kKernelBinned)  // pass 2 writes whole panels too (binned.hip k_bin_acc); not
+        return p.npanels > 0 && p.variant != 51 && p.variant != 52;  // its ablations
     return p.kernel == kKernelSweep && p.sweep_packed && !p.sweep_det && p.sweep_split == 1 && p.npanels > 0 &&
            (p.sweep_variant == 0 || p.sweep_variant == 28);
 }

@@ -184,3 +184,35 @@ def test_streamed_copy_back_with_empty_rows(monkeypatch, capfd, run):
     absax = oracle.spmv_gold(rp, col, np.abs(val), x)
     assert float(np.max(np.abs(y - (y0 + ref)) / (np.abs(y0) + absax + 1e-300))) <= 1e-12
     assert np.array_equal(y[lens == 0], y0[lens == 0])  # empty rows: y_fpga += 0
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("units", [1, 2])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_streamed_copy_back_of_the_binned_kernel(monkeypatch, capfd, units, dtype):
+    """The two-pass binned kernel (config 5's automatic choice in fp32) streams too: its second
+    pass writes whole panels (binned.hip k_bin_acc) and flags each one. Three calls through
+    spmv_hw, y against the oracle each time, tapered pieces, and the same y as the unstreamed
+    merge to rounding (the LDS adds run in timing order)."""
+    monkeypatch.setenv("SPMV_NGPUS", str(units))
+    monkeypatch.setenv("SPMV_HW_MERGE", "host")
+    monkeypatch.setenv("SPMV_HW_TRACE", "1")
+    monkeypatch.setenv("SPMV_HW_KERNEL", "binned")
+    monkeypatch.delenv("SPMV_HW_STREAM", raising=False)
+    lib = spmv_hw.load(dtype)
+    h = _matrix(lib, 6_000_000, 96_000_000)
+    ys = _flow(lib, *h, calls=3)
+    _, err = capfd.readouterr()
+    assert err.count("D2H landed (streamed)") == 3, err[-2000:]
+    _check_tapered_pieces(err, units, calls=3)
+    ref = oracle.spmv_gold(*h) if dtype == np.float64 else oracle.spmv_fp64acc(*h)
+    assert oracle.scaled_error(*h, ref, ys[0]) <= (1e-12 if dtype == np.float64 else 2e-6)
+    for k in (1, 2):
+        d = ys[k].astype(np.float64) - ys[k - 1].astype(np.float64)
+        assert oracle.scaled_error(*h, ref.astype(np.float64), d) <= (1e-12 if dtype == np.float64 else 1e-5)
+    monkeypatch.setenv("SPMV_HW_STREAM", "0")
+    ys0 = _flow(lib, *h, calls=1)
+    _, err = capfd.readouterr()
+    assert "streamed" not in err
+    scale = float(np.abs(ys[0].astype(np.float64)).max())
+    assert float(np.abs(ys0[0].astype(np.float64) - ys[0]).max()) <= (1e-13 if dtype == np.float64 else 1e-5) * scale
