@@ -4,7 +4,6 @@ accum_results '+=' mapping; gather of disjoint slices to rank 0; all-gather of p
 every rank, the iterative-solver form) rebuilding the full y.
 The per-rank product here is the CPU oracle standing in for the GPU kernel (test only)."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -14,13 +13,13 @@ import torch.multiprocessing as mp
 from conftest import ROOT
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _store(tmp_path):
+    """Rendezvous through a file (torch FileStore) in the test's own directory: no TCP port to
+    pick, so parallel test workers cannot collide on one."""
+    return str(tmp_path / "pg_store")
 
 
-def _worker(rank, world, port, mode, q):
+def _worker(rank, world, store, mode, q):
     for p in (ROOT, os.path.join(ROOT, "spmv-fpga_amd"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
     import torch
@@ -30,8 +29,7 @@ def _worker(rank, world, port, mode, q):
     import oracle
     import spmv_hw
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + store, rank=rank, world_size=world)
     try:
         lib = spmv_hw.load(np.float64)
         rng = np.random.default_rng(5)
@@ -101,11 +99,11 @@ def _worker(rank, world, port, mode, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("mode", ["reduce", "gather", "allgather", "pipelined", "dependent"])
-def test_row_sliced_exchange_rebuilds_y(world, mode):
+def test_row_sliced_exchange_rebuilds_y(world, mode, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    store = _store(tmp_path)
+    procs = [ctx.Process(target=_worker, args=(r, world, store, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -117,7 +115,7 @@ def test_row_sliced_exchange_rebuilds_y(world, mode):
     assert sum(counts) == 20_000 and min(counts) > 0
 
 
-def _rank0_worker(rank, world, port, q):
+def _rank0_worker(rank, world, store, q):
     for p in (ROOT, os.path.join(ROOT, "spmv-fpga_amd")):
         sys.path.insert(0, p)
     import time
@@ -126,8 +124,7 @@ def _rank0_worker(rank, world, port, q):
 
     import spmv_dist as sdist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + store, rank=rank, world_size=world)
     try:
         got = []
 
@@ -153,14 +150,14 @@ def _rank0_worker(rank, world, port, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_rank0_only_waits_on_the_store(world):
+def test_rank0_only_waits_on_the_store(world, tmp_path):
     """bench.py's N-unit drop-in run at N > 1: rank 0 alone runs the child (every GPU of the node)
     while the other ranks wait on the process group's store, not in a GPU collective; every rank
     learns whether rank 0's result passed, and a waiting rank gives up after its timeout."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank0_worker, args=(r, world, port, q)) for r in range(world)]
+    store = _store(tmp_path)
+    procs = [ctx.Process(target=_rank0_worker, args=(r, world, store, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -13,7 +13,6 @@ tests execute the same arithmetic without a GPU:
     csr_hw_wrapper.cpp:276-281) on slices of rows.
 The per-rank product here is the CPU oracle standing in for the GPU kernel (test only)."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -137,13 +136,13 @@ def test_schedule_rejects_bad_arguments(lib):
     assert L.spmv_mgpu_schedule(GATHER, 0, 2, bp, None, 0) == 2  # count only
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _store(tmp_path):
+    """Rendezvous through a file (torch FileStore) in the test's own directory: no TCP port to
+    pick, so parallel test workers cannot collide on one."""
+    return str(tmp_path / "pg_store")
 
 
-def _worker(rank, world, port, pattern, q):
+def _worker(rank, world, store, pattern, q):
     for p in (ROOT, os.path.join(ROOT, "spmv-fpga_amd"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
     import torch
@@ -153,8 +152,7 @@ def _worker(rank, world, port, pattern, q):
     import spmv_dist as sdist
     import spmv_hw as hw
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + store, rank=rank, world_size=world)
     try:
         lib = hw.load(np.float64)
         rng = np.random.default_rng(7)
@@ -219,11 +217,11 @@ def _worker(rank, world, port, pattern, q):
 
 @pytest.mark.parametrize("pattern", ["balanced", "empty"])
 @pytest.mark.parametrize("world", [2, 3, 5, 8])
-def test_gloo_replay_of_schedule_matches_oracle(world, pattern):
+def test_gloo_replay_of_schedule_matches_oracle(world, pattern, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, pattern, q)) for r in range(world)]
+    store = _store(tmp_path)
+    procs = [ctx.Process(target=_worker, args=(r, world, store, pattern, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
