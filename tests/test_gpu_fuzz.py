@@ -7,6 +7,8 @@ cancel. Gate as in test_gpu_parity: scaled error <= 1e-12 fp64 / 2e-6 fp32 again
 bitwise against the restated hardware order (spmv.cpp:66-104, csr_hw.cpp:1531-1565) for a
 random VF and column-block width. "auto" and "tune" run the automatic and the timed
 layout choice (SPMV_HW_KERNEL unset / =tune)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -17,7 +19,9 @@ from test_gpu_parity import KERNEL_ID, _bitwise, check, run_device
 
 pytestmark = pytest.mark.gpu
 
-SEEDS = list(range(48))
+# 48 seeds in the suite; SPMV_FUZZ_SEEDS=a-b runs seeds [a, b) instead (one-off extended runs)
+_SR = os.environ.get("SPMV_FUZZ_SEEDS", "0-48").split("-")
+SEEDS = list(range(int(_SR[0]), int(_SR[1])))
 FUZZ_KERNELS = ["tiles", "tiles_wide", "sweep", "sweep_rc", "sweep_unpacked", "sweep_det", "gold", "slices", "slices_wide",
                 "slices_acc32", "fpga", "blocked", "binned", "binned_delta", "auto", "tune"]
 ENV = {"tiles_wide": {"SPMV_TILE_NARROW": "0"}, "sweep_unpacked": {"SPMV_SWEEP_PACKED": "0"},
