@@ -1,5 +1,9 @@
 #!/usr/bin/env bash
-# A/B of two builds of libspmv_hw_f64.so on one box (the headline bench line, interleaved)
+# A/B of two builds of libspmv_hw_f64.so on one box (the headline bench line, interleaved).
+# libspmv_hw_f64_old.so (not tracked) is the product library built from another commit's sources:
+#   git archive <commit> spmv-fpga_amd include | tar -x -C /tmp/old && make -C /tmp/old/spmv-fpga_amd all
+#   cp /tmp/old/spmv-fpga_amd/lib/libspmv_hw_f64.so tools/_ab/libspmv_hw_f64_old.so
+# (./tools/_ab is in .gpurunignore: drop that line to send the copies to the box again)
 set -u
 OUT=gpurun_out/${1:-r06u}; mkdir -p "$OUT"
 cp spmv-fpga_amd/lib/libspmv_hw_f64.so tools/_ab/libspmv_hw_f64_new.so
