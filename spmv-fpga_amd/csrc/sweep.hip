@@ -1486,8 +1486,13 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
     // after a bounded search the cuts are taken at the first P and any panel above the LDS rows is
     // split into panels of at most rmax rows
     const uint64_t P_first = std::max<uint64_t>(1, (n + rmax - 1) / rmax);
+    uint64_t P_start = P_first;
+    // (tools build) SPMV_SWEEP_ROUNDS=k: at least k rounds of whole panels on a matrix that fills
+    // a round anyway (smaller panels: earlier first panels for a streamed copy-back)
+    if (const char *ke = ablation_env("SPMV_SWEEP_ROUNDS"); ke && std::atoi(ke) > 0 && P_first * 2 >= (uint64_t)cus)
+        P_start = std::max<uint64_t>(P_first, (uint64_t)std::min(std::atoi(ke), 8) * cus);
     bool subdivide = false;
-    for (uint64_t P = P_first;; ++P) {
+    for (uint64_t P = P_start;; ++P) {
         {
             // pieces pay when the slice fills at most half the workgroups with full panels and
             // the partial sums (split * n fp64 values, written once and read once by the
@@ -1535,7 +1540,7 @@ int build_sweep(spmv_plan &p, const IndexType *h_rp, const IndexType *d_col_src,
             }
             subdivide = true;
             xbias = 0.0;
-            P = P_first - 1;  // (++P)
+            P = P_start - 1;  // (++P)
         }
     }
     const uint32_t P = (uint32_t)(prow.size() - 1);

@@ -59,7 +59,8 @@ TOOLS_ONLY_ENV = ("SPMV_TILE_XCD", "SPMV_TILE_NARROW", "SPMV_TILE_CLUSTER", "SPM
                   "SPMV_SWEEP_ACC", "SPMV_SWEEP_SPLIT", "SPMV_SWEEP_PIECES", "SPMV_SWEEP_COMBINE",
                   "SPMV_SWEEP_PACKED", "SPMV_SWEEP_LANE_ORDER", "SPMV_HW_BLOCKING_SYNC",
                   "SPMV_HW_PIECES", "SPMV_HW_ADD_SPLIT", "SPMV_HW_ADD_THREADS", "SPMV_GRAPH_FORM",
-                  "SPMV_BEHIND_BLOCKS", "SPMV_BEHIND_ROWS", "SPMV_HW_DIRECT", "SPMV_HW_PIECE_SHAPE")
+                  "SPMV_BEHIND_BLOCKS", "SPMV_BEHIND_ROWS", "SPMV_HW_DIRECT", "SPMV_HW_PIECE_SHAPE",
+                  "SPMV_SWEEP_ROUNDS")
 
 
 def tools_env(monkeypatch, name, value):
