@@ -37,7 +37,8 @@ parity (full-size componentwise-scaled error vs that oracle run; mandatory at ev
 or missing check prints value null / valid false and exits 3), dropin (the drop-in boundary
 itself: create_csr_hw_matrix -> spmv_hw -> verification in a child process, the reference's
 "Matrix read", "Hardware execution", "Result accumulation" and "Total" times; at N > 1 rank 0
-runs it with N units merged by the library's RCCL reduce), value_e2e (2 nnz / (SpMV step +
+runs it with N units merged by the library's RCCL reduce, then with the default host merge,
+dropin.host_merge), value_e2e (2 nnz / (SpMV step +
 the exchange that completes y); = value at N = 1),
 lds_xtiles (power-law, 1 GPU: the same matrix through kernel 4, the reference's dataflow with a
 block of x in LDS per workgroup -- the technique BASELINE configs 3/5 name -- timed beside the
