@@ -1170,7 +1170,8 @@ def value_e2e(out, ms, nnz_all):
     compute-only `value` -- the reference's "Total time" is hardware + accumulation
     (csr_hw_wrapper.cpp:276-285). At N > 1 the exchange is the library's own RCCL reduce of
     full-length partials (spmv_mgpu_run MGPU_REDUCE: accum_results' +=, exchange only, median
-    of 5, max over ranks, verified), else torch.distributed's reduce; at N = 1 there is none."""
+    of 5, max over ranks, verified), else torch.distributed's reduce; at N = 1 there is none. The
+    form also gives the rate with the library's gather of the disjoint slices (with_gather)."""
     if out["n_ranks"] == 1 and not out["dist_rehearsal"]:
         return out["value"], {"form": "one GPU: the SpMV is the whole job (no exchange)"}
     ex = out.get("exchange") if isinstance(out.get("exchange"), dict) else {}
@@ -1181,10 +1182,14 @@ def value_e2e(out, ms, nnz_all):
         ex_ms, src = ex["reduce_ms"], "exchange.reduce_ms (torch.distributed reduce)"
     else:
         return None, {"form": "no exchange was measured"}
-    return (round(2.0 * nnz_all / ((ms + ex_ms) * 1e-3) / 1e9, 3),
-            {"form": "serial SpMV step (ms_per_step) + the y reduce onto rank 0, per SpMV", "ms_per_step": ms,
-             "exchange_ms": ex_ms, "exchange_src": src,
-             "value_is": "compute-only: max-over-ranks SpMV step, no collective inside the timed step"})
+    form = {"form": "serial SpMV step (ms_per_step) + the y reduce onto rank 0, per SpMV", "ms_per_step": ms,
+            "exchange_ms": ex_ms, "exchange_src": src,
+            "value_is": "compute-only: max-over-ranks SpMV step, no collective inside the timed step"}
+    if "gather_exchange_ms" in nat:  # the bandwidth-optimal form beside it (disjoint slices to rank 0)
+        g = nat["gather_exchange_ms"]
+        form["with_gather"] = {"value": round(2.0 * nnz_all / ((ms + g) * 1e-3) / 1e9, 3), "exchange_ms": g,
+                               "exchange_src": "exchange.native.gather_exchange_ms (library RCCL gather, verified)"}
+    return round(2.0 * nnz_all / ((ms + ex_ms) * 1e-3) / 1e9, 3), form
 
 
 def main():

@@ -29,6 +29,10 @@ def test_value_e2e_prefers_the_library_reduce():
     v, form = bench.value_e2e(_out(exchange=ex), 0.12, 160e6)
     assert v == pytest.approx(2 * 160e6 / (0.32e-3) / 1e9, rel=1e-3)
     assert form["exchange_ms"] == 0.2 and "library RCCL reduce" in form["exchange_src"]
+    assert "with_gather" not in form
+    ex["native"]["gather_exchange_ms"] = 0.05
+    v2, form = bench.value_e2e(_out(exchange=ex), 0.12, 160e6)
+    assert v2 == v and form["with_gather"]["value"] == pytest.approx(2 * 160e6 / (0.17e-3) / 1e9, rel=1e-3)
 
 
 def test_value_e2e_falls_back_to_torch_reduce_then_to_none():
