@@ -195,6 +195,25 @@ bool stream_enabled()
     return !(e && e[0] == '0');
 }
 
+// The copy pattern of spmv_hw's merge (`pieces` copies of y into the pinned staging, each followed
+// by its event), run three times on stream s at create time. One whole-y copy alone left the
+// second spmv_hw call's enqueue of the pieces stalling for ~10 ms (and a later one for a few ms)
+// in most processes measured (profiles/r06zu_*): the runtime's first uses of that many copies and
+// events on a stream happen here instead, outside the timed calls.
+void warm_copies(ValueType *stage, const ValueType *d_src, uint64_t rows, uint64_t pieces, hipStream_t s,
+                 d2h_events &done)
+{
+    for (int rep = 0; rep < 3 && rows; ++rep) {
+        for (uint64_t t = 0; t < pieces; ++t) {
+            const uint64_t b = rows * t / pieces, e = rows * (t + 1) / pieces;
+            check(hipMemcpyAsync(stage + b, d_src + b, (e - b) * sizeof(ValueType), hipMemcpyDeviceToHost, s),
+                  "warm D2H");
+            check(hipEventRecord(done.get(t), s), "warm D2H");
+        }
+        check(hipStreamSynchronize(s), "warm D2H");
+    }
+}
+
 // streamed copy-back of unit m (host merge): pinned panel flags the sweep kernel writes, the
 // panels' row bounds on the host and a copy stream (its first large copy run here, like the
 // unit stream's)
@@ -219,9 +238,8 @@ void setup_streaming(hw_matrix_impl *m)
               "hipHostMalloc(direct y)");
         check(hipHostGetDevicePointer((void **)&m->d_direct, m->h_direct, 0), "hipHostGetDevicePointer(direct y)");
     }
-    check(hipMemcpyAsync(m->h_stage, m->d_y, rows * sizeof(ValueType), hipMemcpyDeviceToHost, m->copy_stream),
-          "warm D2H");
-    check(hipStreamSynchronize(m->copy_stream), "warm D2H");
+    m->done.device = m->device;
+    warm_copies(m->h_stage, m->d_y, rows, 8, m->copy_stream, m->done);
 }
 
 int env_pieces(int dflt)
@@ -229,6 +247,7 @@ int env_pieces(int dflt)
     const char *e = ablation_env("SPMV_HW_PIECES");
     return e ? std::max(1, std::atoi(e)) : dflt;
 }
+
 
 // Panel bounds of a streamed copy-back's k pieces over P panels. The copy engine runs the pieces
 // back to back, so what is left when the last copy lands is that piece's host add: the pieces
@@ -643,10 +662,14 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         const IndexType rows = h->row_end - h->row_begin;
         if (rows && merge == kMergeHost) {  // the RCCL merge stages the whole y instead (below)
             alloc_y_scratch(h);
-            // full size: large copies take a different path whose first use costs ~20 ms
+            // full size first (large copies take a different path whose first use costs ~20 ms),
+            // then the merge's own pieces
             check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
                   "warm D2H");
             check(hipStreamSynchronize(us), "warm D2H");
+            h->done.device = h->device;
+            warm_copies(h->h_stage, h->d_y, rows, rows < (1u << 18) ? 1 : std::max(2, env_pieces(8) / units), us,
+                        h->done);
             setup_streaming(h);
         }
         spmv_plan_stats st;
@@ -708,6 +731,8 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
                                  unit_stream(0)),
                   "warm D2H");
             check(hipStreamSynchronize(unit_stream(0)), "warm D2H");
+            c->done.device = c->devices[0];
+            warm_copies(c->h_full, mgpu_root_y(c->mg), n, n < (1u << 18) ? 1 : env_pieces(8), unit_stream(0), c->done);
         }
         impl((*hw_matrix)[0])->clique = c;
     }
