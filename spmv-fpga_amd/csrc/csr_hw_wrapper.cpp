@@ -195,11 +195,13 @@ bool stream_enabled()
     return !(e && e[0] == '0');
 }
 
-// The copy pattern of spmv_hw's merge (`pieces` copies of y into the pinned staging, each followed
-// by its event), run three times on stream s at create time. One whole-y copy alone left the
-// second spmv_hw call's enqueue of the pieces stalling for ~10 ms (and a later one for a few ms)
-// in most processes measured (profiles/r06zu_*): the runtime's first uses of that many copies and
-// events on a stream happen here instead, outside the timed calls.
+// The copy pattern of spmv_hw's unstreamed host merge (`pieces` copies of y into the pinned
+// staging, each followed by its event), run three times on the unit's stream at create time for
+// plans that do not stream their copy-back. One whole-y warm copy alone left the second
+// spmv_hw call's enqueue of the pieces stalling for ~10 ms (and a later one for a few ms) in most
+// processes measured (profiles/r06zu_*, r06zv_*): the runtime's first uses of that many copies
+// and events on a stream happen here instead. Streamed plans (copies on their own stream) never
+// showed it and skip this (it adds ~25 ms to create_csr_hw_matrix at 10M rows).
 void warm_copies(ValueType *stage, const ValueType *d_src, uint64_t rows, uint64_t pieces, hipStream_t s,
                  d2h_events &done)
 {
@@ -238,8 +240,9 @@ void setup_streaming(hw_matrix_impl *m)
               "hipHostMalloc(direct y)");
         check(hipHostGetDevicePointer((void **)&m->d_direct, m->h_direct, 0), "hipHostGetDevicePointer(direct y)");
     }
-    m->done.device = m->device;
-    warm_copies(m->h_stage, m->d_y, rows, 8, m->copy_stream, m->done);
+    check(hipMemcpyAsync(m->h_stage, m->d_y, rows * sizeof(ValueType), hipMemcpyDeviceToHost, m->copy_stream),
+          "warm D2H");
+    check(hipStreamSynchronize(m->copy_stream), "warm D2H");
 }
 
 int env_pieces(int dflt)
@@ -667,10 +670,12 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
             check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
                   "warm D2H");
             check(hipStreamSynchronize(us), "warm D2H");
-            h->done.device = h->device;
-            warm_copies(h->h_stage, h->d_y, rows, rows < (1u << 18) ? 1 : std::max(2, env_pieces(8) / units), us,
-                        h->done);
             setup_streaming(h);
+            if (!h->h_flags) {  // a plan whose copy-back waits for the kernel: its own pieces too
+                h->done.device = h->device;
+                warm_copies(h->h_stage, h->d_y, rows, rows < (1u << 18) ? 1 : std::max(2, env_pieces(8) / units), us,
+                            h->done);
+            }
         }
         spmv_plan_stats st;
         spmv_plan_get_stats(h->plan, &st);
@@ -731,8 +736,6 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
                                  unit_stream(0)),
                   "warm D2H");
             check(hipStreamSynchronize(unit_stream(0)), "warm D2H");
-            c->done.device = c->devices[0];
-            warm_copies(c->h_full, mgpu_root_y(c->mg), n, n < (1u << 18) ? 1 : env_pieces(8), unit_stream(0), c->done);
         }
         impl((*hw_matrix)[0])->clique = c;
     }
