@@ -657,26 +657,38 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         h->device = unit_device(u);
         h->row_begin = bounds[u];
         h->row_end = bounds[u + 1];
+        const double tp = timestamp_us();
         if (spmv_plan_create_host(&h->plan, h->device, matrix, h->row_begin, h->row_end))
             die(std::string("create_csr_hw_matrix: ") + spmv_hw_last_error());
+        if (trace)
+            std::fprintf(stderr, "spmv_hw trace: unit %d %-21s %9.3f ms\n", u, "plan", (timestamp_us() - tp) / 1000);
+        const double ts = timestamp_us();
         // stream, y buffers and the first D2H copy (copy-engine setup, ~8 ms) happen here, not
         // inside spmv_hw's timed region
         const hipStream_t us = unit_stream(u);
         const IndexType rows = h->row_end - h->row_begin;
         if (rows && merge == kMergeHost) {  // the RCCL merge stages the whole y instead (below)
             alloc_y_scratch(h);
+            const double ta = timestamp_us();
             // full size first (large copies take a different path whose first use costs ~20 ms),
             // then the merge's own pieces
             check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
                   "warm D2H");
             check(hipStreamSynchronize(us), "warm D2H");
+            const double tw = timestamp_us();
             setup_streaming(h);
+            if (trace)
+                std::fprintf(stderr, "spmv_hw trace: unit %d y staging alloc %.3f, warm copy %.3f, streaming setup %.3f ms\n",
+                             u, (ta - ts) / 1000, (tw - ta) / 1000, (timestamp_us() - tw) / 1000);
             if (!h->h_flags) {  // a plan whose copy-back waits for the kernel: its own pieces too
                 h->done.device = h->device;
                 warm_copies(h->h_stage, h->d_y, rows, rows < (1u << 18) ? 1 : std::max(2, env_pieces(8) / units), us,
                             h->done);
             }
         }
+        if (trace)
+            std::fprintf(stderr, "spmv_hw trace: unit %d %-21s %9.3f ms\n", u, "y staging + copy warm-up",
+                         (timestamp_us() - ts) / 1000);
         spmv_plan_stats st;
         spmv_plan_get_stats(h->plan, &st);
         const spmv_plan &pl = *h->plan;
@@ -792,6 +804,7 @@ void create_csr_hw_x_vector(csr_hw_vector **hw_x, csr_vector *x, int blocks, Ind
         die("create_csr_hw_x_vector: blocks must be hw_matrix[0]->blocks (1)");
     if (x->nr_values > nr_cols[0])
         die("create_csr_hw_x_vector: x is longer than the matrix has columns");
+    const double tx = timestamp_us();
     const int units = std::max(g_units_max, spmv_hw_units());
     const int ndev = std::min(units, device_count());
     auto *v = new hw_vector_impl();
@@ -812,6 +825,8 @@ void create_csr_hw_x_vector(csr_hw_vector **hw_x, csr_vector *x, int blocks, Ind
     v->pub.nr_values = v->nr_values;
     v->pub.blocks = 1;
     *hw_x = &v->pub;
+    if (std::getenv("SPMV_HW_TRACE"))
+        std::fprintf(stderr, "spmv_hw trace: %-28s %9.3f ms\n", "x upload", (timestamp_us() - tx) / 1000);
 }
 
 // csr_hw_wrapper.cpp:193-288
