@@ -163,9 +163,11 @@ void alloc_y_scratch(hw_matrix_impl *m)
 {
     const uint64_t rows = m->row_end - m->row_begin;
     check(hipSetDevice(m->device), "hipSetDevice");
-    check(hipMalloc((void **)&m->d_y, rows * sizeof(ValueType)), "hipMalloc(y)");
-    check(hipHostMalloc((void **)&m->h_stage, rows * sizeof(ValueType), hipHostMallocDefault),
-          "hipHostMalloc(y stage)");
+    if (!m->d_y)  // (create_csr_hw_matrix makes both while the plan builds)
+        check(hipMalloc((void **)&m->d_y, rows * sizeof(ValueType)), "hipMalloc(y)");
+    if (!m->h_stage)
+        check(hipHostMalloc((void **)&m->h_stage, rows * sizeof(ValueType), hipHostMallocDefault),
+              "hipHostMalloc(y stage)");
 }
 
 uint64_t ceil16(uint64_t bytes) { return (bytes + 15) / 16; }
@@ -222,8 +224,14 @@ void warm_copies(ValueType *stage, const ValueType *d_src, uint64_t rows, uint64
 void setup_streaming(hw_matrix_impl *m)
 {
     const spmv_plan &pl = *m->plan;
-    if (!sweep_can_flag_panels(pl) || m->row_end == m->row_begin)
+    if (!sweep_can_flag_panels(pl) || m->row_end == m->row_begin) {
+        if (m->copy_stream) {  // (created ahead by create_csr_hw_matrix; not needed)
+            check(hipSetDevice(m->device), "hipSetDevice");
+            (void)hipStreamDestroy(m->copy_stream);
+            m->copy_stream = nullptr;
+        }
         return;
+    }
     check(hipSetDevice(m->device), "hipSetDevice");
     m->panel_rows.resize(pl.npanels + 1);
     check(hipMemcpy(m->panel_rows.data(), pl.d_panel_row, (pl.npanels + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost),
@@ -232,7 +240,8 @@ void setup_streaming(hw_matrix_impl *m)
           "hipHostMalloc(panel flags)");
     std::memset(m->h_flags, 0, pl.npanels * sizeof(uint32_t));
     check(hipHostGetDevicePointer((void **)&m->d_flags, m->h_flags, 0), "hipHostGetDevicePointer(panel flags)");
-    check(hipStreamCreateWithFlags(&m->copy_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!m->copy_stream)  // (else made by create_csr_hw_matrix while the plan built)
+        check(hipStreamCreateWithFlags(&m->copy_stream, hipStreamNonBlocking), "hipStreamCreate");
     const uint64_t rows = m->row_end - m->row_begin;
     if (ablation_env("SPMV_HW_DIRECT") && pl.kernel == kKernelSweep) {  // the measurement form: y straight
                                                                          // into host memory (sweep only)
@@ -658,28 +667,45 @@ void create_csr_hw_matrix(csr_matrix *matrix, csr_hw_matrix ***hw_matrix, bool *
         h->row_begin = bounds[u];
         h->row_end = bounds[u + 1];
         const double tp = timestamp_us();
-        if (spmv_plan_create_host(&h->plan, h->device, matrix, h->row_begin, h->row_end))
+        // the host merge's y scratch (device y, pinned staging) and its copy stream are made on a
+        // helper thread while the plan builds (at 10M fp64 rows: ~27 ms against the plan's ~95;
+        // the first large D2H copies stay after the build, where they do not slow its upload)
+        hipError_t prep_err = hipSuccess;
+        std::thread prep;
+        if (h->row_end > h->row_begin && merge == kMergeHost) {
+            prep = std::thread([h, &prep_err] {
+                const size_t bytes = size_t(h->row_end - h->row_begin) * sizeof(ValueType);
+                hipError_t e = hipSetDevice(h->device);
+                if (e == hipSuccess)
+                    e = hipMalloc((void **)&h->d_y, bytes);
+                if (e == hipSuccess)
+                    e = hipHostMalloc((void **)&h->h_stage, bytes, hipHostMallocDefault);
+                if (e == hipSuccess)
+                    e = hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking);
+                prep_err = e;
+            });
+        }
+        const int plan_rc = spmv_plan_create_host(&h->plan, h->device, matrix, h->row_begin, h->row_end);
+        if (prep.joinable())
+            prep.join();
+        if (plan_rc)
             die(std::string("create_csr_hw_matrix: ") + spmv_hw_last_error());
+        check(prep_err, "create_csr_hw_matrix: y staging");
         if (trace)
             std::fprintf(stderr, "spmv_hw trace: unit %d %-21s %9.3f ms\n", u, "plan", (timestamp_us() - tp) / 1000);
         const double ts = timestamp_us();
-        // stream, y buffers and the first D2H copy (copy-engine setup, ~8 ms) happen here, not
-        // inside spmv_hw's timed region
+        // the streamed copy-back's panel flags, or an unstreamed plan's piece warm-up, here (the y
+        // buffers and the first D2H copies were made while the plan built): none of it inside
+        // spmv_hw's timed region
         const hipStream_t us = unit_stream(u);
         const IndexType rows = h->row_end - h->row_begin;
         if (rows && merge == kMergeHost) {  // the RCCL merge stages the whole y instead (below)
-            alloc_y_scratch(h);
-            const double ta = timestamp_us();
-            // full size first (large copies take a different path whose first use costs ~20 ms),
-            // then the merge's own pieces
+            alloc_y_scratch(h);  // (made by the helper above)
+            // full size first (large copies take a different path whose first use costs ~20 ms)
             check(hipMemcpyAsync(h->h_stage, h->d_y, size_t(rows) * sizeof(ValueType), hipMemcpyDeviceToHost, us),
                   "warm D2H");
             check(hipStreamSynchronize(us), "warm D2H");
-            const double tw = timestamp_us();
             setup_streaming(h);
-            if (trace)
-                std::fprintf(stderr, "spmv_hw trace: unit %d y staging alloc %.3f, warm copy %.3f, streaming setup %.3f ms\n",
-                             u, (ta - ts) / 1000, (tw - ta) / 1000, (timestamp_us() - tw) / 1000);
             if (!h->h_flags) {  // a plan whose copy-back waits for the kernel: its own pieces too
                 h->done.device = h->device;
                 warm_copies(h->h_stage, h->d_y, rows, rows < (1u << 18) ? 1 : std::max(2, env_pieces(8) / units), us,
